@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the path-tracing hot path on the BASELINE.json
+headline config (Cornell 800x800, spp=256, depth=16), 1..N GPUs.
+
+One step = one full-image render (every pixel x spp paths) with the scene and
+camera already resident in HBM, plus - for N > 1 - the RCCL reduce that
+assembles the tile-interleaved framebuffer on rank 0. Rank 0 prints one JSON
+line. Launch N > 1 with torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "mcp-raytracer_amd"))
+
+METRIC = "Msamples/sec (w×h×spp/s) Cornell 800×800 spp=256 @1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+SCENES = {
+    "cornell": ({"type": "cornell"}, {}),
+    "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}}, {"aspect": 1}),
+    "rain": ({"type": "rain", "options": {"seed": 42}}, {}),
+    "default": ({"type": "default"}, {}),
+}
+
+
+def algorithmic_bytes(c: dict, pixels: int) -> float:
+    """32 B/node + 16 B/sphere test + 64 B/quad or plane test +
+    32 B/material fetch + per diffuse bounce per light (64 quad | 16 sphere)
+    + 12 B/pixel accumulator write."""
+    return (32.0 * c["node"] + 16.0 * c["sphere"] + 64.0 * c["quad"] + 64.0 * c["plane"]
+            + 32.0 * c["material"] + 64.0 * c["light_quad"] + 16.0 * c["light_sphere"] + 12.0 * pixels)
+
+
+def cpu_baseline(scene_data, ropts, width, height, spp, target_s=15.0):
+    """The CPU restatement (oracle, ref precision, 1 thread) on a bounded row
+    subsample of the same workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+
+    pyoracle.build()
+    t0 = time.perf_counter()
+    pyoracle.render(scene_data, ropts, region=(0, height // 2, width, 1), threads=1)
+    t_row = max(time.perf_counter() - t0, 1e-3)
+    rows = max(1, min(height, int(target_s / t_row)))
+    step = max(1, height // rows)
+    t0 = time.perf_counter()
+    out = pyoracle.render(scene_data, ropts, row_step=step, threads=1)
+    dt = time.perf_counter() - t0
+    samples = out["stats"]["samples"]["total"]
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": f"rows j%{step}==0 of the {width}x{height} image at spp={spp} "
+                      f"({int(out['stats']['pixels'])} px, {int(samples)} samples, {dt:.1f} s), "
+                      f"oracle/oracle.cpp ref precision, single thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scene", default="cornell", choices=sorted(SCENES))
+    ap.add_argument("--width", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--depth", type=int, default=16)
+    ap.add_argument("--precision", default="ref", choices=["ref", "fp32"])
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "pmc_traffic.json"),
+                    help="JSON with measured HBM bytes per launch (from rocprofv3 --pmc)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from raytracer_amd import _build
+
+    if rank == 0 or world == 1:
+        _build.build_native()
+    if world > 1:
+        dist.barrier()
+    import raytracer_amd as rt
+
+    cfg, extra = SCENES[args.scene]
+    scene_data = rt.generate_scene_data(cfg)
+    ropts = {"width": args.width, "samples": args.spp, "depth": args.depth, "aTolerance": 0,
+             "seed": args.seed, "precision": args.precision, **extra}
+    cam = rt.create_camera_from_scene_data(scene_data, ropts)
+    W, H = cam.image_width, cam.image_height
+    dev = torch.device("cuda", local_rank)
+    frame = torch.zeros((H, W, 3), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    # Algorithmic work of this rank's launch: one instrumented (untimed) launch;
+    # identical seeds => identical paths to every timed launch.
+    _, counters = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world,
+                                    stream=sptr, synchronize=True, count_work=True)
+    st, _ = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr,
+                              synchronize=True)
+    my_pixels = int(st.pixels)
+    bytes_per_launch = algorithmic_bytes(counters, my_pixels)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(k=None):
+        frame.zero_()
+        if k is not None:
+            ev[k][0].record(stream)
+        cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr)
+        if k is not None:
+            ev[k][1].record(stream)
+        if world > 1:
+            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1)
+
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms_max = float(t[0]), float(t[1])
+
+    samples_per_step = W * H * args.spp
+    value = samples_per_step * args.steps / elapsed / 1e6
+    achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9  # this rank's GB/s
+    traffic = None
+    tf = Path(args.traffic_file)
+    if tf.exists():
+        try:
+            td = json.loads(tf.read_text())
+            key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n{world}"
+            traffic = td.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(scene_data, {k: v for k, v in ropts.items() if k != "precision"}, W, H, args.spp)
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f64" if args.precision == "ref" else "f32",
+            "data": "synthetic: reference scene generator output (deterministic), path RNG seed "
+                    f"{args.seed:#x}; no datasets",
+            "config": {"workload": f"{args.scene} {W}x{H} spp={args.spp} depth={args.depth}",
+                       "scene": args.scene, "width": W, "height": H, "spp": args.spp, "depth": args.depth,
+                       "precision": args.precision, "adaptive": False,
+                       "parallelism": f"8x8-tile interleave x{world} + RCCL reduce to rank 0"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "pt_render_kernel", "kernel_ms": round(kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "work_per_sample": {k: round(v / max(counters["samples"], 1), 3)
+                                             for k, v in counters.items()}},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

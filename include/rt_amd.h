@@ -1,0 +1,143 @@
+/*
+ * rt_amd.h - C ABI of the MI355X path-tracing core (librt_amd.so).
+ *
+ * This is the drop-in boundary for df07/mcp-raytracer's hot path. The
+ * reference has no FFI: its boundary is the TypeScript object model, and the
+ * call site this library replaces is
+ *
+ *     createCameraFromSceneData(sceneData, renderOptions)   src/scenes/scenes.ts:60-104
+ *     camera.renderRegion(buffer, region) -> RenderStats     src/camera.ts:388-431
+ *     camera.render(buffer)                                  src/camera.ts:439-446
+ *
+ * called from generateImageBuffer (src/raytracer.ts:56-59) and from each render
+ * worker (src/render-utils/renderWorker.ts:17-26). Scenes cross the boundary in
+ * the reference's own wire format, SceneData JSON (src/scenes/sceneData.ts:8-110);
+ * render options are the RenderOptions object (src/camera.ts:42-52) as JSON, plus
+ * two extensions: "seed" (u32 path-RNG seed; the reference's Math.random is
+ * unseeded) and "precision" ("ref" = JS-double scalars, the default; "fp32").
+ *
+ * Conventions: plain pointers and sizes, no torch types. Every function returns
+ * 0 on success and a nonzero status on failure; rt_last_error() then holds the
+ * message (thread-local), mirroring the reference's thrown Error messages.
+ * Host-side functions (scene generation, camera build, info, export) run without
+ * a GPU; render functions need a visible gfx950 device.
+ */
+#ifndef RT_AMD_H
+#define RT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_AMD_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID = 1,   /* bad arguments / scene (reference throws an Error) */
+    RT_ERR_DEVICE = 2,    /* HIP error */
+    RT_ERR_RENDER = 3     /* error raised during rendering (e.g. miss without background) */
+};
+
+enum { RT_PRECISION_REF = 0, RT_PRECISION_FP32 = 1 };
+
+typedef struct rt_camera rt_camera;
+
+/* RenderRegion (src/camera.ts:54-59) */
+typedef struct {
+    int32_t x, y, width, height;
+} rt_region;
+
+/* RenderStats (src/render-utils/renderStats.ts:6-19). min fields are +inf when
+ * no pixel / sample was rendered, exactly as the reference's Infinity seed. */
+typedef struct {
+    double pixels;
+    double samples_total, samples_min, samples_max, samples_avg;
+    double bounces_total, bounces_min, bounces_max, bounces_avg;
+} rt_render_stats;
+
+/* Camera geometry and options after createCameraFromSceneData. */
+typedef struct {
+    int32_t width, height, channels;
+    int32_t n_objects, n_nodes, n_lights, n_materials, bvh_depth;
+    int32_t samples_loop, depth, roulette, roulette_depth, mode, adaptive, precision;
+    uint32_t seed;
+    double samples, aperture, a_tolerance, a_batch;
+} rt_camera_info;
+
+/* Device-resident launch (benchmarks, multi-GPU). Output pointers are DEVICE
+ * pointers in full-frame layout (width*height*3, row-major, RGB) and only the
+ * region's tiles are written. Tiles are 8x8 pixel blocks enumerated row-major
+ * over the region; this launch renders tile t iff t % tile_groups == tile_group
+ * (tile_groups = 1: the whole region). `stream` is a hipStream_t (NULL = default). */
+typedef struct {
+    rt_region region;
+    int32_t tile_group, tile_groups;
+    int32_t precision;       /* -1: the camera's precision */
+    int32_t count_work;      /* 1: instrumented build, fills work_counters */
+    uint8_t* rgb;            /* device, may be NULL */
+    float* radiance;         /* device, may be NULL */
+    int32_t* px_samples;     /* device W*H, may be NULL */
+    int32_t* px_bounces;     /* device W*H, may be NULL */
+    void* stream;
+    int32_t synchronize;     /* 1: wait and fill stats / work_counters; 0: asynchronous */
+} rt_launch;
+
+/* Work counters of an instrumented launch (SURVEY.md §8d algorithmic bytes). */
+enum {
+    RT_CT_NODE = 0, RT_CT_SPHERE, RT_CT_QUAD, RT_CT_PLANE, RT_CT_MATERIAL, RT_CT_LIGHT_QUAD,
+    RT_CT_LIGHT_SPHERE, RT_CT_BOUNCES, RT_CT_DIFFUSE, RT_CT_SAMPLES, RT_CT_RAYS, RT_CT_WORDS
+};
+
+int rt_version(void);
+const char* rt_last_error(void);
+void rt_free(void* p);
+
+/* generateSceneData({type, options}) (src/scenes/scenes.ts:42-50). type is
+ * "default" | "spheres" | "rain" | "cornell"; options_json the *SceneOptions
+ * object or NULL. *out_json is malloc'ed; release with rt_free. */
+int rt_generate_scene_data(const char* type, const char* options_json, char** out_json);
+
+/* createCameraFromSceneData (src/scenes/scenes.ts:60-104). Host only. */
+int rt_camera_create(const char* scene_json, const char* render_options_json, rt_camera** out);
+void rt_camera_destroy(rt_camera* cam);
+int rt_camera_get_info(const rt_camera* cam, rt_camera_info* info);
+int rt_camera_set_precision(rt_camera* cam, int32_t precision);
+
+/* Camera.renderRegion (src/camera.ts:388-431). rgb: caller-owned HOST buffer of
+ * width*height*3 bytes (Uint8ClampedArray layout), only the region is written.
+ * radiance: optional host float buffer of width*height*3 (final pixel colour).
+ * stats: optional. */
+int rt_camera_render_region(rt_camera* cam, const rt_region* region, uint8_t* rgb, float* radiance,
+                            rt_render_stats* stats);
+/* Camera.render (src/camera.ts:439-446): the whole image. */
+int rt_camera_render(rt_camera* cam, uint8_t* rgb, float* radiance, rt_render_stats* stats);
+
+/* Device-resident render (see rt_launch). stats / work_counters (RT_CT_WORDS
+ * u64) are filled only when launch->synchronize is 1. */
+int rt_camera_render_device(rt_camera* cam, const rt_launch* launch, rt_render_stats* stats,
+                            uint64_t* work_counters);
+
+/* Host copies of the flattened scene, for tests: sizes in bytes are
+ * n_nodes*32, n_objects*96, n_materials*64, n_lights*16; prim_object gets
+ * n_objects int32 (leaf slot -> SceneData.objects index). Any pointer may be NULL. */
+int rt_camera_export(const rt_camera* cam, void* nodes, void* prims, void* materials, void* lights,
+                     int32_t* prim_object);
+
+/* Closest hit of n rays through the device BVH (ref precision). orig/dir: host
+ * float[3*n]; out: host double[10*n] = {hit, t, p.xyz, n.xyz, front, prim_slot}. */
+int rt_debug_world_hit(rt_camera* cam, int32_t n, const float* orig, const float* dir, double* out);
+
+/* The path RNG stream (seeded Math.random replacement), host evaluation. */
+int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out);
+
+/* Number of visible HIP devices (0 without a GPU). */
+int rt_device_count(int32_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_AMD_H */

@@ -1,0 +1,724 @@
+// The path-tracing hot path as one persistent HIP kernel for gfx950.
+//
+// Restates, per lane, Camera.renderRegion's pixel loop (src/camera.ts:388-431)
+// with getRay (176-210), the rayColor recursion turned into a bounce loop
+// (221-319), BVH traversal (src/geometry/bvh.ts:128-146, aabb.ts:30-55,
+// hittableList.ts:71-87), sphere/quad/plane intersection (src/entities/*),
+// material scatter (src/materials/*), the mixture-PDF light sampling
+// (src/geometry/pdf.ts) and the spp accumulate (src/render-utils/renderStats.ts:76-88).
+//
+// Work decomposition (MI355X): a wave owns an 8x8 pixel tile, one pixel per
+// lane; waves pull tiles from a global atomic counter (persistent grid, load
+// balanced across the 256 CUs / 8 XCDs). Each lane renders its pixel's samples
+// in order - the reference accumulates samples sequentially in fp32, so the
+// per-pixel order is part of the result - but lanes are NOT synchronised per
+// sample: a lane whose path terminates immediately starts its next sample in
+// the same loop trip (path regeneration), so the wave runs for
+// max_lane(sum of path lengths), not sum_samples(max_lane(path length)).
+// The BVH traversal stack lives in LDS, lane-interleaved ([depth][lane]) so
+// every push/pop is a conflict-free ds_write/ds_read_b32.
+//
+// Numerics: `Real` = double restates the reference exactly (fp64 scalars,
+// fp32 vector stores; built with -ffp-contract=off); Real = float is the fp32
+// fast mode. See rt_math.hpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rt_math.hpp"
+#include "scene.hpp"
+
+namespace rt {
+
+struct DevScene {
+    const RtNode* __restrict__ nodes;
+    const RtPrim* __restrict__ prims;
+    const RtMat* __restrict__ mats;
+    const RtLight* __restrict__ lights;
+    RtCamera cam;
+    double mix_total;  // MixturePDF.totalWeight for [0.5, 0.5/nL x nL]
+    double light_w;    // 0.5 / nL
+};
+
+// Stats words (u64): pixels, samples total, samples min, samples max,
+// bounces total, bounces min, bounces max, error flags.
+enum { ST_PIXELS = 0, ST_SAMPLES, ST_SMIN, ST_SMAX, ST_BOUNCES, ST_BMIN, ST_BMAX, ST_ERROR, ST_WORDS };
+// Instrumentation words (u64): the algorithmic-work counts of SURVEY.md §8d.
+enum {
+    CT_NODE = 0, CT_SPHERE, CT_QUAD, CT_PLANE, CT_MATERIAL, CT_LIGHT_QUAD, CT_LIGHT_SPHERE,
+    CT_BOUNCES, CT_DIFFUSE, CT_SAMPLES, CT_RAYS, CT_WORDS
+};
+enum : unsigned long long { ERR_NO_BACKGROUND = 1ull, ERR_EMIT_STACK = 2ull };
+
+struct RenderOut {
+    uint8_t* rgb;        // W*H*3 (full frame layout), may be null
+    float* radiance;     // W*H*3, may be null
+    int32_t* px_samples; // W*H, may be null
+    int32_t* px_bounces; // W*H, may be null
+    unsigned long long* stats;     // ST_WORDS
+    unsigned long long* counters;  // CT_WORDS (COUNT builds only)
+    unsigned int* tile_counter;
+};
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kTile = 8;          // 8x8 pixels per wave-tile
+constexpr int kEmitStack = 128;   // emission terms kept for the right fold (EMIT builds)
+
+// ---------------------------------------------------------------------------
+// Seeded replacement for Math.random: PCG32 (XSH-RR) stream per (seed, pixel,
+// sample), consumed in the reference's draw order.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rng_init(uint32_t seed, uint32_t pixel, uint32_t sample) {
+    return splitmix64((((uint64_t)pixel << 32) | sample) ^ splitmix64(seed));
+}
+__device__ __forceinline__ uint32_t rng_u32(uint64_t& s) {
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+template <class Real> __device__ __forceinline__ Real uniform(uint64_t& s);
+template <> __device__ __forceinline__ double uniform<double>(uint64_t& s) {
+    return (double)rng_u32(s) * (1.0 / 4294967296.0);
+}
+template <> __device__ __forceinline__ float uniform<float>(uint64_t& s) {
+    return (float)(rng_u32(s) >> 8) * (1.0f / 16777216.0f);
+}
+
+// Math.* on the scalar type.
+__device__ __forceinline__ double m_cos(double x) { return ::cos(x); }
+__device__ __forceinline__ float m_cos(float x) { return ::cosf(x); }
+__device__ __forceinline__ double m_sin(double x) { return ::sin(x); }
+__device__ __forceinline__ float m_sin(float x) { return ::sinf(x); }
+__device__ __forceinline__ double m_pow(double x, double y) { return ::pow(x, y); }
+__device__ __forceinline__ float m_pow(float x, float y) { return ::powf(x, y); }
+__device__ __forceinline__ double m_abs(double x) { return ::fabs(x); }
+__device__ __forceinline__ float m_abs(float x) { return ::fabsf(x); }
+__device__ __forceinline__ double m_sqrt(double x) { return ::sqrt(x); }
+__device__ __forceinline__ float m_sqrt(float x) { return ::sqrtf(x); }
+
+template <class Real> struct K {
+    static constexpr Real PI = (Real)3.141592653589793;
+    static constexpr Real TMIN = (Real)0.001;
+};
+
+__device__ __forceinline__ V3 ld3(const float* p) { return V3{p[0], p[1], p[2]}; }
+
+// Per-ray constants reused by every node and primitive test.
+template <class Real> struct RayK {
+    V3 o, d;
+    Real inv[3];  // 1/d[a] (AABB.hit computes it per node; same value)
+    Real a;       // d.lengthSquared() (Sphere.hit computes it per sphere; same value)
+};
+
+template <class Real>
+__device__ __forceinline__ RayK<Real> make_ray(V3 o, V3 d) {
+    RayK<Real> r;
+    r.o = o;
+    r.d = d;
+    r.inv[0] = (Real)1 / (Real)d.x;
+    r.inv[1] = (Real)1 / (Real)d.y;
+    r.inv[2] = (Real)1 / (Real)d.z;
+    r.a = len2<Real>(d);
+    return r;
+}
+
+// AABB.hit (src/geometry/aabb.ts:30-55): each axis is clipped against the
+// ORIGINAL interval (the reference does not carry tMin/tMax across axes);
+// comparisons keep the reference's NaN behaviour.
+template <class Real>
+__device__ __forceinline__ bool box_hit(const RtNode& n, const RayK<Real>& r, Real tmin, Real tmax) {
+    const float o[3] = {r.o.x, r.o.y, r.o.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const Real invD = r.inv[a];
+        Real t0 = ((Real)n.bmin[a] - (Real)o[a]) * invD;
+        Real t1 = ((Real)n.bmax[a] - (Real)o[a]) * invD;
+        if (invD < (Real)0) { Real tmp = t0; t0 = t1; t1 = tmp; }
+        const Real lo = t0 > tmin ? t0 : tmin;
+        const Real hi = t1 < tmax ? t1 : tmax;
+        if (hi <= lo) return false;
+    }
+    return true;
+}
+
+template <class Real> __device__ __forceinline__ Real sphere_radius(const RtPrim& p);
+template <> __device__ __forceinline__ double sphere_radius<double>(const RtPrim& p) { return p.s0; }
+template <> __device__ __forceinline__ float sphere_radius<float>(const RtPrim& p) { return p.g0[3]; }
+template <class Real> __device__ __forceinline__ Real plane_d(const RtPrim& p);
+template <> __device__ __forceinline__ double plane_d<double>(const RtPrim& p) { return p.s0; }
+template <> __device__ __forceinline__ float plane_d<float>(const RtPrim& p) { return p.g0[3]; }
+
+// Sphere.hit root selection (src/entities/sphere.ts:45-65); returns t only.
+template <class Real>
+__device__ __forceinline__ bool sphere_t(const RtPrim& p, const RayK<Real>& r, Real tmin, Real tmax, Real& t) {
+    const V3 c = ld3(p.g0);
+    const Real rad = sphere_radius<Real>(p);
+    const V3 oc = sub(r.o, c);
+    const Real halfB = dot<Real>(oc, r.d);
+    const Real cc = len2<Real>(oc) - rad * rad;
+    const Real disc = halfB * halfB - r.a * cc;
+    if (disc < (Real)0) return false;
+    const Real sq = m_sqrt(disc);
+    Real root = (-halfB - sq) / r.a;
+    if (!(tmin < root && root < tmax)) {
+        root = (-halfB + sq) / r.a;
+        if (!(tmin < root && root < tmax)) return false;
+    }
+    t = root;
+    return true;
+}
+
+// Plane.intersect (src/entities/plane.ts:55-77) + Quad bounds (quad.ts:50-76).
+template <class Real, bool QUAD>
+__device__ __forceinline__ bool planar_t(const RtPrim& p, const RayK<Real>& r, Real tmin, Real tmax, Real& t) {
+    const V3 n = ld3(p.g3);
+    const Real denom = dot<Real>(n, r.d);
+    if (m_abs(denom) < (Real)1e-8) return false;
+    const Real tt = (plane_d<Real>(p) - dot<Real>(n, r.o)) / denom;
+    if (!(tmin < tt && tt < tmax)) return false;
+    if (QUAD) {
+        const V3 ip = ray_at<Real>(r.o, r.d, tt);
+        const V3 ph = sub(ip, ld3(p.g0));
+        const V3 w = ld3(p.g4);
+        const Real alpha = dot<Real>(w, cross<Real>(ph, ld3(p.g2)));
+        const Real beta = dot<Real>(w, cross<Real>(ld3(p.g1), ph));
+        if (alpha < (Real)0 || alpha > (Real)1 || beta < (Real)0 || beta > (Real)1) return false;
+    }
+    t = tt;
+    return true;
+}
+
+template <class Real, bool COUNT>
+__device__ __forceinline__ bool prim_t(const RtPrim& p, const RayK<Real>& r, Real tmin, Real tmax, Real& t,
+                                       uint32_t* cnt) {
+    if (p.type == PRIM_SPHERE) {
+        if (COUNT) cnt[CT_SPHERE]++;
+        return sphere_t<Real>(p, r, tmin, tmax, t);
+    }
+    if (p.type == PRIM_QUAD) {
+        if (COUNT) cnt[CT_QUAD]++;
+        return planar_t<Real, true>(p, r, tmin, tmax, t);
+    }
+    if (COUNT) cnt[CT_PLANE]++;
+    return planar_t<Real, false>(p, r, tmin, tmax, t);
+}
+
+// BVHNode.hit restated as an explicit DFS with the same visiting order: the
+// box is tested when a node is entered with the closest-so-far interval, left
+// subtree before right, leaf primitives in leaf order with a narrowing max.
+// `stk` points at this lane's column of the LDS stack (stride kBlock ints).
+template <class Real, bool COUNT>
+__device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
+                                           uint32_t* cnt) {
+    const Real tmin = K<Real>::TMIN;
+    Real tmax = (Real)__builtin_inf();
+    int hit = -1;
+    int sp = 0;
+    int node = 0;
+    while (true) {
+        const RtNode nd = S.nodes[node];
+        if (COUNT) cnt[CT_NODE]++;
+        bool descend = false;
+        if (box_hit<Real>(nd, r, tmin, tmax)) {
+            if (nd.b < 0) {
+                const int end = nd.a - nd.b;
+                for (int k = nd.a; k < end; ++k) {
+                    Real t;
+                    if (prim_t<Real, COUNT>(S.prims[k], r, tmin, tmax, t, cnt)) {
+                        tmax = t;
+                        hit = k;
+                    }
+                }
+            } else {
+                stk[sp * kBlock] = nd.b;
+                ++sp;
+                node = nd.a;
+                descend = true;
+            }
+        }
+        if (!descend) {
+            if (sp == 0) break;
+            --sp;
+            node = stk[sp * kBlock];
+        }
+    }
+    t_hit = tmax;
+    return hit;
+}
+
+// ONBasis (src/geometry/onbasis.ts:18-51)
+struct Onb {
+    V3 u, v, w;
+};
+template <class Real>
+__device__ __forceinline__ Onb make_onb(V3 n) {
+    Onb b;
+    b.w = unit<Real>(n);
+    const V3 a = m_abs((Real)b.w.x) > (Real)0.9 ? v3(0, 1, 0) : v3(1, 0, 0);
+    b.v = unit<Real>(cross<Real>(b.w, a));
+    b.u = cross<Real>(b.w, b.v);
+    return b;
+}
+template <class Real>
+__device__ __forceinline__ V3 onb_local(const Onb& b, V3 a) {
+    return add(add(scale<Real>(b.u, (Real)a.x), scale<Real>(b.v, (Real)a.y)), scale<Real>(b.w, (Real)a.z));
+}
+
+// Vec3.randomInUnitSphere (src/geometry/vec3.ts:285-292): 3 draws per try.
+template <class Real>
+__device__ __forceinline__ V3 random_in_unit_sphere(uint64_t& rng) {
+    while (true) {
+        const Real x = (Real)-1 + (Real)2 * uniform<Real>(rng);
+        const Real y = (Real)-1 + (Real)2 * uniform<Real>(rng);
+        const Real z = (Real)-1 + (Real)2 * uniform<Real>(rng);
+        const V3 p = mk<Real>(x, y, z);
+        if (len2<Real>(p) < (Real)1) return p;
+    }
+}
+
+// Dielectric.scatter direction (src/materials/dielectric.ts:44-98). Draws one
+// random only when refraction is possible (short-circuit ||).
+template <class Real>
+__device__ __forceinline__ V3 dielectric_dir(Real ior, bool front, V3 din, V3 n, uint64_t& rng, bool& reflected) {
+    const Real ratio = front ? ((Real)1 / ior) : ior;
+    const V3 ud = unit<Real>(din);
+    const Real cosT = js_min<Real>(dot<Real>(neg(ud), n), (Real)1);
+    const Real sinT = m_sqrt((Real)1 - cosT * cosT);
+    const bool cannot = ratio * sinT > (Real)1;
+    bool refl = cannot;
+    if (!refl) {
+        Real r0 = ((Real)1 - ratio) / ((Real)1 + ratio);
+        r0 = r0 * r0;
+        const Real reflectance = r0 + ((Real)1 - r0) * m_pow((Real)1 - cosT, (Real)5);
+        refl = reflectance > uniform<Real>(rng);
+    }
+    reflected = refl;
+    if (refl) return reflect<Real>(ud, n);
+    // Vec3.refract (src/geometry/vec3.ts:193-209)
+    const V3 perp = scale<Real>(add(ud, scale<Real>(n, cosT)), ratio);
+    const V3 par = scale<Real>(n, -m_sqrt(m_abs((Real)1 - len2<Real>(perp))));
+    return add(perp, par);
+}
+
+enum ScatterKind { SC_NONE = 0, SC_SPEC = 1, SC_PDF = 2 };
+
+// Material.scatter over the flat material table; Mixed and Layered follow
+// their children iteratively (mixedMaterial.ts:38-44, layeredMaterial.ts:36-53).
+template <class Real>
+__device__ __forceinline__ int scatter(const DevScene& S, int mi, V3 din, V3 n, bool front, uint64_t& rng, V3& att,
+                                       V3& dir) {
+    while (true) {
+        const RtMat m = S.mats[mi];
+        switch (m.type) {
+            case MAT_LAMBERT:
+                att = ld3(m.color);
+                return SC_PDF;
+            case MAT_METAL: {
+                const V3 refl = reflect<Real>(unit<Real>(din), n);
+                const Real fuzz = (Real)m.p0;
+                V3 f = refl;
+                if (fuzz > (Real)0) f = add(refl, scale<Real>(random_in_unit_sphere<Real>(rng), fuzz));
+                if (dot<Real>(f, n) <= (Real)0) return SC_NONE;
+                att = ld3(m.color);
+                dir = f;
+                return SC_SPEC;
+            }
+            case MAT_GLASS: {
+                bool r;
+                dir = dielectric_dir<Real>((Real)m.p0, front, din, n, rng, r);
+                att = v3(1, 1, 1);
+                return SC_SPEC;
+            }
+            case MAT_MIXED:
+                mi = uniform<Real>(rng) < (Real)m.p0 ? m.c0 : m.c1;
+                continue;
+            case MAT_LAYERED: {
+                bool r;
+                const V3 d2 = dielectric_dir<Real>((Real)S.mats[m.c0].p0, front, din, n, rng, r);
+                if (r) {
+                    att = v3(1, 1, 1);
+                    dir = d2;
+                    return SC_SPEC;
+                }
+                din = d2;  // the refracted ray becomes rIn for the inner material
+                mi = m.c1;
+                continue;
+            }
+            default:  // MAT_LIGHT and DefaultMaterial: no scatter
+                return SC_NONE;
+        }
+    }
+}
+
+// Quad.pdfValue / Sphere.pdfValue (quad.ts:123-140, sphere.ts:106-131):
+// re-intersect the light on (0.001, inf), not occlusion-aware.
+template <class Real, bool COUNT>
+__device__ __forceinline__ Real light_pdf_value(const DevScene& S, const RtLight& L, V3 origin, V3 dir,
+                                                uint32_t* cnt) {
+    const RtPrim p = S.prims[L.prim];
+    const RayK<Real> r = make_ray<Real>(origin, dir);
+    Real t;
+    if (L.type == PRIM_QUAD) {
+        if (COUNT) cnt[CT_LIGHT_QUAD]++;
+        if (!planar_t<Real, true>(p, r, K<Real>::TMIN, (Real)__builtin_inf(), t)) return (Real)0;
+        const V3 hp = ray_at<Real>(origin, dir, t);
+        const V3 n = ld3(p.g3);
+        const bool front = dot<Real>(dir, n) <= (Real)0;
+        const V3 hn = front ? n : neg(n);
+        const Real d2 = len2<Real>(sub(hp, origin));
+        const Real cosine = m_abs(dot<Real>(dir, hn));
+        return d2 / ((Real)L.area * cosine);
+    }
+    if (COUNT) cnt[CT_LIGHT_SPHERE]++;
+    if (!sphere_t<Real>(p, r, K<Real>::TMIN, (Real)__builtin_inf(), t)) return (Real)0;
+    const Real rad = sphere_radius<Real>(p);
+    const Real d2 = len2<Real>(sub(ld3(p.g0), origin));
+    if (d2 <= rad * rad) return (Real)1 / ((Real)4 * K<Real>::PI);
+    const Real cosT = m_sqrt((Real)1 - rad * rad / d2);
+    const Real solid = (Real)2 * K<Real>::PI * ((Real)1 - cosT);
+    return (Real)1 / solid;
+}
+
+// Quad.pdfRandomVec / Sphere.pdfRandomVec (quad.ts:148-158, sphere.ts:140-147)
+template <class Real>
+__device__ __forceinline__ V3 light_generate(const DevScene& S, const RtLight& L, V3 origin, uint64_t& rng) {
+    const RtPrim p = S.prims[L.prim];
+    if (L.type == PRIM_QUAD) {
+        const Real alpha = uniform<Real>(rng);
+        const Real beta = uniform<Real>(rng);
+        const V3 rp = add(add(ld3(p.g0), scale<Real>(ld3(p.g1), alpha)), scale<Real>(ld3(p.g2), beta));
+        return unit<Real>(sub(rp, origin));
+    }
+    const V3 oc = sub(ld3(p.g0), origin);
+    const Real d2 = len2<Real>(oc);
+    const Onb b = make_onb<Real>(oc);
+    // Vec3.randomToSphere (src/geometry/vec3.ts:345-351)
+    const Real rad = sphere_radius<Real>(p);
+    const Real r1 = uniform<Real>(rng);
+    const Real r2 = uniform<Real>(rng);
+    const Real z = (Real)1 + r2 * (m_sqrt((Real)1 - rad * rad / d2) - (Real)1);
+    const Real phi = (Real)2 * K<Real>::PI * r1;
+    const Real s = m_sqrt((Real)1 - z * z);
+    return onb_local<Real>(b, mk<Real>(m_cos(phi) * s, m_sin(phi) * s, z));
+}
+
+// CosinePDF.value (src/geometry/pdf.ts:43-46)
+template <class Real>
+__device__ __forceinline__ Real cosine_value(const Onb& b, V3 dir) {
+    const Real c = dot<Real>(unit<Real>(dir), b.w);
+    return c <= (Real)0 ? (Real)0 : c / K<Real>::PI;
+}
+
+// writeColorToBuffer (src/camera.ts:455-472) into a Uint8ClampedArray.
+__device__ __forceinline__ uint8_t to_u8(float c) {
+    const double r = ::sqrt((double)c);
+    const double v = ::floor(255.999 * r);
+    if (!(v > 0.0)) return 0;
+    if (v >= 255.0) return 255;
+    return (uint8_t)v;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_min(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { unsigned long long x = __shfl_xor(v, o, 64); v = x < v ? x : v; }
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { unsigned long long x = __shfl_xor(v, o, 64); v = x > v ? x : v; }
+    return v;
+}
+
+// pixelConverged (src/camera.ts:348-368), in JS doubles.
+__device__ __forceinline__ bool pixel_converged(const RtCamera& c, int n, double sIll, double sIll2) {
+    if (c.a_tolerance <= 0.0 || c.samples <= 1.0 || n < 2) return false;
+    const double rem = ::fmod((double)n, c.a_batch);
+    if (rem != 0.0) return false;  // also NaN
+    const double mean = sIll / n;
+    const double var = (sIll2 - (sIll * sIll) / n) / (n - 1);
+    if (var <= 0.0 || var != var) return true;
+    const double ci = 1.96 * ::sqrt(var) / ::sqrt((double)n);
+    return ci <= c.a_tolerance * mean;
+}
+
+template <class Real, bool EMIT, bool COUNT>
+__global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion reg, RenderOut out, int tiles_x,
+                                                           int my_tiles) {
+    extern __shared__ int lds_stack[];
+    const RtCamera& C = S.cam;
+    const int lane = threadIdx.x & (kWave - 1);
+    int* stk = lds_stack + threadIdx.x;
+
+    const int endX = min(reg.x + reg.width, C.width);
+    const int endY = min(reg.y + reg.height, C.height);
+
+    uint32_t cnt[CT_WORDS];
+    if (COUNT) {
+#pragma unroll
+        for (int k = 0; k < CT_WORDS; ++k) cnt[k] = 0;
+    }
+    unsigned long long st_pixels = 0, st_samples = 0, st_smin = ~0ull, st_smax = 0, st_b = 0, st_bmin = ~0ull,
+                       st_bmax = 0, st_err = 0;
+
+    while (true) {
+        unsigned int tile = 0;
+        if (lane == 0) tile = atomicAdd(out.tile_counter, 1u);
+        tile = __shfl(tile, 0, 64);
+        if ((int)tile >= my_tiles) break;
+        const int gt = reg.tile_group + (int)tile * reg.tile_groups;
+        const int i = reg.x + (gt % tiles_x) * kTile + (lane & (kTile - 1));
+        const int j = reg.y + (gt / tiles_x) * kTile + (lane / kTile);
+        bool active = i < endX && j < endY && C.n_samples > 0;
+        const bool valid_px = i < endX && j < endY;
+        const uint32_t pix = (uint32_t)j * (uint32_t)C.width + (uint32_t)i;
+
+        // PixelStats (src/render-utils/renderStats.ts:66-88)
+        V3 color = v3(0, 0, 0);
+        int n = 0;
+        unsigned long long bsum = 0;
+        int bmin = 0x7fffffff, bmax = 0;
+        double sIll = 0.0, sIll2 = 0.0;
+
+        // path state
+        bool new_path = true;
+        uint64_t rng = 0;
+        V3 o = v3(0, 0, 0), d = v3(0, 0, 0), T = v3(1, 1, 1);
+        int bounces = 0;
+        V3 em[EMIT ? kEmitStack : 1];
+        int em_n = 0;
+
+        while (active) {
+            if (new_path) {
+                rng = rng_init(C.seed, pix, (uint32_t)n);
+                // getRay (src/camera.ts:176-210)
+                const V3 p00 = ld3(C.pixel00), du = ld3(C.du), dv = ld3(C.dv), cen = ld3(C.center);
+                const V3 pc = add(add(p00, scale<Real>(du, (Real)i)), scale<Real>(dv, (Real)j));
+                V3 ps = pc;
+                if (C.samples > 1.0) {
+                    const Real px = (Real)-0.5 + uniform<Real>(rng);
+                    const Real py = (Real)-0.5 + uniform<Real>(rng);
+                    ps = add(add(pc, scale<Real>(du, px)), scale<Real>(dv, py));
+                }
+                o = cen;
+                d = sub(ps, cen);
+                if (C.aperture > 0.0) {
+                    V3 rd;
+                    while (true) {  // Vec3.randomInUnitDisk (vec3.ts:357-364)
+                        const Real a = (Real)2 * uniform<Real>(rng) - (Real)1;
+                        const Real b = (Real)2 * uniform<Real>(rng) - (Real)1;
+                        rd = mk<Real>(a, b, (Real)0);
+                        if (len2<Real>(rd) < (Real)1) break;
+                    }
+                    const V3 off = add(scale<Real>(ld3(C.ddu), (Real)rd.x), scale<Real>(ld3(C.ddv), (Real)rd.y));
+                    o = add(cen, off);
+                    d = sub(ps, o);
+                }
+                T = v3(1, 1, 1);
+                bounces = 0;
+                em_n = 0;
+                new_path = false;
+            }
+
+            // ---- one rayColor level (src/camera.ts:221-319) ----
+            bool term = false;
+            V3 c = v3(0, 0, 0);
+            if (bounces >= C.depth) {
+                term = true;
+            } else {
+                if (C.roulette && bounces >= C.roulette_depth) {
+                    const Real mc = js_max<Real>(js_max<Real>((Real)T.x, (Real)T.y), (Real)T.z);
+                    const Real p = js_min<Real>(mc, (Real)0.95);
+                    if (uniform<Real>(rng) > p) term = true;
+                    else T = divs<Real>(T, p);
+                }
+                if (!term) {
+                    const RayK<Real> ray = make_ray<Real>(o, d);
+                    Real t;
+                    if (COUNT) cnt[CT_RAYS]++;
+                    const int h = closest_hit<Real, COUNT>(S, ray, t, stk, cnt);
+                    if (h < 0) {
+                        term = true;
+                        if (!C.has_background) st_err |= ERR_NO_BACKGROUND;
+                        const V3 ud = unit<Real>(d);
+                        const Real a = (Real)0.5 * ((Real)ud.y + (Real)1);
+                        c = mulv(add(scale<Real>(ld3(C.bg_top), (Real)1 - a), scale<Real>(ld3(C.bg_bottom), a)), T);
+                    } else {
+                        if (COUNT) cnt[CT_MATERIAL]++;
+                        // hit record (sphere.ts:67-84, quad.ts:72-83, plane.ts:246-259)
+                        const RtPrim pr = S.prims[h];
+                        const V3 p = ray_at<Real>(o, d, t);
+                        V3 nrm;
+                        bool front;
+                        if (pr.type == PRIM_SPHERE) {
+                            nrm = divs<Real>(sub(p, ld3(pr.g0)), sphere_radius<Real>(pr));
+                            front = dot<Real>(d, nrm) <= (Real)0;
+                            if (!front) nrm = neg(nrm);
+                        } else {
+                            const V3 pn = ld3(pr.g3);
+                            front = dot<Real>(d, pn) <= (Real)0;
+                            nrm = front ? pn : neg(pn);
+                        }
+                        const RtMat hm = S.mats[pr.mat];
+                        const V3 emitted = mulv(ld3(hm.emitted), T);
+                        V3 att, sdir;
+                        const int kind = scatter<Real>(S, pr.mat, d, nrm, front, rng, att, sdir);
+                        if (kind == SC_NONE) {
+                            term = true;
+                            c = emitted;
+                        } else {
+                            ++bounces;
+                            if (kind == SC_SPEC) {
+                                T = mulv(T, att);
+                                o = p;
+                                d = sdir;
+                            } else {
+                                if (COUNT) cnt[CT_DIFFUSE]++;
+                                // MixturePDF([CosinePDF(n), light pdfs...], [0.5, 0.5/nL...])
+                                const Onb b = make_onb<Real>(nrm);
+                                const Real total = (Real)S.mix_total;
+                                const Real lw = (Real)S.light_w;
+                                const Real rnd = uniform<Real>(rng) * total;
+                                Real partial = (Real)0.5;
+                                V3 gdir;
+                                if (rnd < partial || C.n_lights == 0) {
+                                    const Real r1 = uniform<Real>(rng);
+                                    const Real r2 = uniform<Real>(rng);
+                                    const Real phi = (Real)2 * K<Real>::PI * r1;
+                                    const Real sr2 = m_sqrt(r2);
+                                    gdir = onb_local<Real>(
+                                        b, mk<Real>(m_cos(phi) * sr2, m_sin(phi) * sr2, m_sqrt((Real)1 - r2)));
+                                } else {
+                                    int pick = C.n_lights - 1;
+                                    for (int l = 0; l < C.n_lights; ++l) {
+                                        partial += lw;
+                                        if (rnd < partial) { pick = l; break; }
+                                    }
+                                    gdir = light_generate<Real>(S, S.lights[pick], p, rng);
+                                }
+                                const Real cv = cosine_value<Real>(b, gdir);
+                                Real sum = (Real)0.5 * cv;
+                                for (int l = 0; l < C.n_lights; ++l)
+                                    sum += lw * light_pdf_value<Real, COUNT>(S, S.lights[l], p, gdir, cnt);
+                                const Real pv = sum / total;
+                                if (pv <= (Real)0.0001) {
+                                    term = true;
+                                    c = emitted;
+                                } else {
+                                    const V3 brdf = scale<Real>(att, cv);
+                                    T = divs<Real>(mulv(T, brdf), pv);
+                                    o = p;
+                                    d = gdir;
+                                }
+                            }
+                            if (EMIT && !term) {
+                                if (em_n < kEmitStack) em[em_n] = emitted;
+                                else st_err |= ERR_EMIT_STACK;
+                                ++em_n;
+                            }
+                        }
+                    }
+                }
+            }
+
+            if (term) {
+                // emitted.add(rayColor(...)) at every level: a right fold.
+                if (EMIT) {
+                    for (int k = min(em_n, kEmitStack) - 1; k >= 0; --k) c = add(em[k], c);
+                }
+                // PixelStats.add (renderStats.ts:76-88)
+                color = add(color, c);
+                ++n;
+                bsum += (unsigned long long)bounces;
+                bmin = min(bmin, bounces);
+                bmax = max(bmax, bounces);
+                if (C.adaptive) {
+                    const double il = illuminance(c);
+                    sIll += il;
+                    sIll2 += il * il;
+                }
+                if (COUNT) {
+                    cnt[CT_SAMPLES]++;
+                    cnt[CT_BOUNCES] += (uint32_t)bounces;
+                }
+                if (n >= C.n_samples || pixel_converged(C, n, sIll, sIll2)) active = false;
+                else new_path = true;
+            }
+        }
+
+        if (valid_px) {
+            // finalColor (src/camera.ts:326-340)
+            V3 fin;
+            if (C.mode == MODE_BOUNCES) {
+                const double avg = n > 0 ? (double)bsum / (double)n : 0.0;
+                fin = mk<double>(0.0, 0.0, js_min<double>(avg / (double)C.depth_raw, 1.0));
+            } else if (C.mode == MODE_SAMPLES) {
+                fin = mk<double>(js_min<double>((double)n / C.samples, 1.0), 0.0, 0.0);
+            } else {
+                fin = divs<double>(color, (double)n);
+            }
+            const size_t off = (size_t)pix * 3;
+            if (out.radiance) {
+                out.radiance[off] = fin.x;
+                out.radiance[off + 1] = fin.y;
+                out.radiance[off + 2] = fin.z;
+            }
+            if (out.rgb) {
+                out.rgb[off] = to_u8(fin.x);
+                out.rgb[off + 1] = to_u8(fin.y);
+                out.rgb[off + 2] = to_u8(fin.z);
+            }
+            if (out.px_samples) out.px_samples[pix] = n;
+            if (out.px_bounces) out.px_bounces[pix] = (int32_t)bsum;
+            st_pixels += 1;
+            st_samples += (unsigned long long)n;
+            st_smin = min(st_smin, (unsigned long long)n);
+            st_smax = max(st_smax, (unsigned long long)n);
+            st_b += bsum;
+            if (n > 0) st_bmin = min(st_bmin, (unsigned long long)bmin);
+            st_bmax = max(st_bmax, (unsigned long long)bmax);
+        }
+    }
+
+    // RenderStats.addPixel / merge (renderStats.ts:21-64): one atomic per wave.
+    const unsigned long long sp = wave_sum(st_pixels), ss = wave_sum(st_samples), sb = wave_sum(st_b);
+    const unsigned long long smn = wave_min(st_smin), smx = wave_max(st_smax);
+    const unsigned long long bmn = wave_min(st_bmin), bmx = wave_max(st_bmax);
+    unsigned long long err = st_err;
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) err |= __shfl_xor(err, k, 64);
+    if (lane == 0 && sp > 0) {
+        atomicAdd(&out.stats[ST_PIXELS], sp);
+        atomicAdd(&out.stats[ST_SAMPLES], ss);
+        atomicMin(&out.stats[ST_SMIN], smn);
+        atomicMax(&out.stats[ST_SMAX], smx);
+        atomicAdd(&out.stats[ST_BOUNCES], sb);
+        atomicMin(&out.stats[ST_BMIN], bmn);
+        atomicMax(&out.stats[ST_BMAX], bmx);
+    }
+    if (lane == 0 && err) atomicOr(&out.stats[ST_ERROR], err);
+    if (COUNT) {
+#pragma unroll
+        for (int k = 0; k < CT_WORDS; ++k) {
+            const unsigned long long v = wave_sum((unsigned long long)cnt[k]);
+            if (lane == 0 && v) atomicAdd(&out.counters[k], v);
+        }
+    }
+}
+
+}  // namespace rt

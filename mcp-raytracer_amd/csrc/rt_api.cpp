@@ -1,0 +1,413 @@
+// C ABI of the path-tracing core (include/rt_amd.h).
+//
+// rt_camera = the reference's Camera object after createCameraFromSceneData:
+// the host build (scene.cpp) plus lazily allocated device copies. Rendering
+// follows Camera.renderRegion's contract: the caller owns the output buffer,
+// only the region is written, RenderStats are returned.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_amd.h"
+#include "json.hpp"
+#include "launch.hpp"
+#include "scene.hpp"
+
+using namespace rt;
+
+namespace {
+
+thread_local std::string g_error;
+
+int set_error(int code, const std::string& msg) {
+    g_error = msg;
+    return code;
+}
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int device_cus(int dev) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    return cus;
+}
+
+}  // namespace
+
+struct rt_camera {
+    SceneBuild build;
+    int32_t precision = PREC_REF;
+    double mix_total = 0.5, light_w = 0.0;
+    std::mutex mu;
+
+    int device = -1;
+    RtNode* d_nodes = nullptr;
+    RtPrim* d_prims = nullptr;
+    RtMat* d_mats = nullptr;
+    RtLight* d_lights = nullptr;
+    unsigned long long* d_stats = nullptr;
+    unsigned long long* d_counters = nullptr;
+    unsigned int* d_tile = nullptr;
+    uint8_t* d_rgb = nullptr;
+    float* d_rad = nullptr;
+    int cus = 256;
+
+    ~rt_camera() { release(); }
+
+    void release() {
+        if (device < 0) return;
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(device);
+        for (void* p : {(void*)d_nodes, (void*)d_prims, (void*)d_mats, (void*)d_lights, (void*)d_stats,
+                        (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad})
+            if (p) (void)hipFree(p);
+        (void)hipSetDevice(prev);
+        device = -1;
+    }
+
+    template <class T>
+    static T* upload(const std::vector<T>& v) {
+        T* p = nullptr;
+        const size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(T);
+        hip_check(hipMalloc(&p, bytes), "hipMalloc");
+        if (!v.empty()) hip_check(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+        return p;
+    }
+
+    void ensure_device() {
+        int dev = 0;
+        hip_check(hipGetDevice(&dev), "hipGetDevice");
+        if (device == dev) return;
+        if (device >= 0) release();
+        d_nodes = upload(build.nodes);
+        d_prims = upload(build.prims);
+        d_mats = upload(build.mats);
+        d_lights = upload(build.lights);
+        hip_check(hipMalloc(&d_stats, ST_WORDS * sizeof(unsigned long long)), "hipMalloc");
+        hip_check(hipMalloc(&d_counters, CT_WORDS * sizeof(unsigned long long)), "hipMalloc");
+        hip_check(hipMalloc(&d_tile, 64), "hipMalloc");
+        device = dev;
+        cus = device_cus(dev);
+    }
+
+    void ensure_frame() {
+        if (d_rgb) return;
+        const size_t px = (size_t)build.cam.width * build.cam.height;
+        hip_check(hipMalloc(&d_rgb, std::max<size_t>(px * 3, 1)), "hipMalloc");
+        hip_check(hipMalloc(&d_rad, std::max<size_t>(px * 3, 1) * sizeof(float)), "hipMalloc");
+    }
+
+    DevScene dev_scene() const {
+        DevScene S;
+        S.nodes = d_nodes;
+        S.prims = d_prims;
+        S.mats = d_mats;
+        S.lights = d_lights;
+        S.cam = build.cam;
+        S.mix_total = mix_total;
+        S.light_w = light_w;
+        return S;
+    }
+
+    // Launch one render; returns after queueing (and synchronising if asked).
+    void launch(const rt_region& region, int tile_group, int tile_groups, int prec, bool count, uint8_t* rgb,
+                float* rad, int32_t* pxs, int32_t* pxb, hipStream_t stream) {
+        const RtCamera& C = build.cam;
+        if (tile_groups < 1 || tile_group < 0 || tile_group >= tile_groups)
+            throw std::invalid_argument("tile_group must satisfy 0 <= tile_group < tile_groups");
+        const int x0 = std::max(region.x, 0), y0 = std::max(region.y, 0);
+        const int x1 = std::min(region.x + region.width, C.width);
+        const int y1 = std::min(region.y + region.height, C.height);
+        RtRegion reg{x0, y0, std::max(x1 - x0, 0), std::max(y1 - y0, 0), tile_group, tile_groups};
+        const int tiles_x = (reg.width + kTile - 1) / kTile;
+        const int tiles_y = (reg.height + kTile - 1) / kTile;
+        const long total = (long)tiles_x * tiles_y;
+        const long mine = total > tile_group ? (total - tile_group + tile_groups - 1) / tile_groups : 0;
+        LaunchGeom g;
+        g.tiles_x = std::max(tiles_x, 1);
+        g.my_tiles = (int)mine;
+        const long want = (mine + (kBlock / kWave) - 1) / (kBlock / kWave);
+        g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus * 8));
+        g.lds_bytes = (size_t)std::max(C.stack_depth, 1) * kBlock * sizeof(int);
+        RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile};
+        hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
+        if (mine == 0) return;
+        const DevScene S = dev_scene();
+        const bool emit = C.emissive_scatter != 0;
+        hipError_t e = prec == PREC_FP32 ? launch_render_fp32(emit, count, S, reg, out, g, stream)
+                                         : launch_render_ref(emit, count, S, reg, out, g, stream);
+        hip_check(e, "pt_render_kernel launch");
+    }
+
+    void read_stats(rt_render_stats* st, uint64_t* counters, hipStream_t stream) {
+        unsigned long long w[ST_WORDS];
+        hip_check(hipMemcpyAsync(w, d_stats, sizeof w, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
+        unsigned long long c[CT_WORDS];
+        if (counters)
+            hip_check(hipMemcpyAsync(c, d_counters, sizeof c, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
+        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        if (counters)
+            for (int k = 0; k < CT_WORDS; ++k) counters[k] = c[k];
+        if (w[ST_ERROR] & ERR_NO_BACKGROUND)
+            throw std::runtime_error("Cannot read properties of undefined (reading 'top')");
+        if (w[ST_ERROR] & ERR_EMIT_STACK)
+            throw std::runtime_error("emission stack overflow: depth exceeds the emissive-scatter limit (128)");
+        if (!st) return;
+        st->pixels = (double)w[ST_PIXELS];
+        st->samples_total = (double)w[ST_SAMPLES];
+        st->samples_min = w[ST_SMIN] == ~0ull ? INFINITY : (double)w[ST_SMIN];
+        st->samples_max = (double)w[ST_SMAX];
+        st->samples_avg = st->pixels > 0 ? st->samples_total / st->pixels : 0.0;
+        st->bounces_total = (double)w[ST_BOUNCES];
+        st->bounces_min = w[ST_BMIN] == ~0ull ? INFINITY : (double)w[ST_BMIN];
+        st->bounces_max = (double)w[ST_BMAX];
+        st->bounces_avg = st->samples_total > 0 ? st->bounces_total / st->samples_total : 0.0;
+    }
+};
+
+extern "C" {
+
+int rt_version(void) { return RT_AMD_VERSION; }
+
+const char* rt_last_error(void) { return g_error.c_str(); }
+
+void rt_free(void* p) { std::free(p); }
+
+int rt_generate_scene_data(const char* type, const char* options_json, char** out_json) {
+    try {
+        if (!type || !out_json) return set_error(RT_ERR_INVALID, "type and out_json are required");
+        rtj::Value opts;
+        const rtj::Value* optp = nullptr;
+        if (options_json && options_json[0]) {
+            opts = rtj::parse(options_json, std::strlen(options_json));
+            if (!opts.is_null()) optp = &opts;
+        }
+        const std::string s = rtj::dump(generate_scene_data(type, optp));
+        char* buf = (char*)std::malloc(s.size() + 1);
+        if (!buf) return set_error(RT_ERR_INVALID, "out of memory");
+        std::memcpy(buf, s.c_str(), s.size() + 1);
+        *out_json = buf;
+        return RT_OK;
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_INVALID, e.what());
+    }
+}
+
+int rt_camera_create(const char* scene_json, const char* render_options_json, rt_camera** out) {
+    try {
+        if (!scene_json || !out) return set_error(RT_ERR_INVALID, "scene_json and out are required");
+        const rtj::Value scene = rtj::parse(scene_json, std::strlen(scene_json));
+        rtj::Value ro;
+        const rtj::Value* rop = nullptr;
+        if (render_options_json && render_options_json[0]) {
+            ro = rtj::parse(render_options_json, std::strlen(render_options_json));
+            if (!ro.is_null()) rop = &ro;
+        }
+        auto* cam = new rt_camera();
+        try {
+            cam->build = build_scene(scene, rop);
+            int32_t prec = PREC_REF;
+            auto pick = [&](const rtj::Value* v) {
+                if (v && v->is_string()) {
+                    if (v->str == "fp32") prec = PREC_FP32;
+                    else if (v->str == "ref") prec = PREC_REF;
+                    else throw std::runtime_error("precision must be 'ref' or 'fp32'");
+                }
+            };
+            if (const rtj::Value* r = scene.get("render")) pick(r->get("precision"));
+            if (rop) pick(rop->get("precision"));
+            cam->precision = prec;
+            // MixturePDF([cosine, ...lights], [0.5, ...0.5/nL]).totalWeight (pdf.ts:48-52)
+            const int nl = cam->build.cam.n_lights;
+            cam->light_w = nl > 0 ? 0.5 / (double)nl : 0.0;
+            double total = 0.0;
+            total += 0.5;
+            for (int k = 0; k < nl; ++k) total += cam->light_w;
+            cam->mix_total = total;
+        } catch (...) {
+            delete cam;
+            throw;
+        }
+        *out = cam;
+        return RT_OK;
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_INVALID, e.what());
+    }
+}
+
+void rt_camera_destroy(rt_camera* cam) { delete cam; }
+
+int rt_camera_get_info(const rt_camera* cam, rt_camera_info* info) {
+    if (!cam || !info) return set_error(RT_ERR_INVALID, "null argument");
+    const RtCamera& C = cam->build.cam;
+    info->width = C.width;
+    info->height = C.height;
+    info->channels = 3;
+    info->n_objects = C.n_prims;
+    info->n_nodes = C.n_nodes;
+    info->n_lights = C.n_lights;
+    info->n_materials = C.n_mats;
+    info->bvh_depth = cam->build.bvh_depth;
+    info->samples_loop = C.n_samples;
+    info->depth = C.depth;
+    info->roulette = C.roulette;
+    info->roulette_depth = C.roulette_depth;
+    info->mode = C.mode;
+    info->adaptive = C.adaptive;
+    info->precision = cam->precision;
+    info->seed = C.seed;
+    info->samples = C.samples;
+    info->aperture = C.aperture;
+    info->a_tolerance = C.a_tolerance;
+    info->a_batch = C.a_batch;
+    return RT_OK;
+}
+
+int rt_camera_set_precision(rt_camera* cam, int32_t precision) {
+    if (!cam) return set_error(RT_ERR_INVALID, "null camera");
+    if (precision != PREC_REF && precision != PREC_FP32) return set_error(RT_ERR_INVALID, "bad precision");
+    cam->precision = precision;
+    return RT_OK;
+}
+
+int rt_camera_render_region(rt_camera* cam, const rt_region* region, uint8_t* rgb, float* radiance,
+                            rt_render_stats* stats) {
+    if (!cam || !region) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    try {
+        cam->ensure_device();
+        cam->ensure_frame();
+        const RtCamera& C = cam->build.cam;
+        const hipStream_t stream = nullptr;
+        cam->launch(*region, 0, 1, cam->precision, false, rgb ? cam->d_rgb : nullptr,
+                    radiance ? cam->d_rad : nullptr, nullptr, nullptr, stream);
+        cam->read_stats(stats, nullptr, stream);
+        // copy back only the region's rows/columns (the caller's buffer is the full frame)
+        const int x0 = std::max(region->x, 0), y0 = std::max(region->y, 0);
+        const int x1 = std::min(region->x + region->width, C.width);
+        const int y1 = std::min(region->y + region->height, C.height);
+        if (x1 > x0 && y1 > y0) {
+            const size_t pitch = (size_t)C.width * 3;
+            const size_t off = ((size_t)y0 * C.width + x0) * 3;
+            const size_t w = (size_t)(x1 - x0) * 3;
+            if (rgb)
+                hip_check(hipMemcpy2D(rgb + off, pitch, cam->d_rgb + off, pitch, w, y1 - y0, hipMemcpyDeviceToHost),
+                          "hipMemcpy2D");
+            if (radiance)
+                hip_check(hipMemcpy2D(radiance + off, pitch * sizeof(float), cam->d_rad + off, pitch * sizeof(float),
+                                      w * sizeof(float), y1 - y0, hipMemcpyDeviceToHost),
+                          "hipMemcpy2D");
+        }
+        return RT_OK;
+    } catch (const HipError& e) {
+        return set_error(RT_ERR_DEVICE, e.what());
+    } catch (const std::invalid_argument& e) {
+        return set_error(RT_ERR_INVALID, e.what());
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_RENDER, e.what());
+    }
+}
+
+int rt_camera_render(rt_camera* cam, uint8_t* rgb, float* radiance, rt_render_stats* stats) {
+    if (!cam) return set_error(RT_ERR_INVALID, "null camera");
+    rt_region r{0, 0, cam->build.cam.width, cam->build.cam.height};
+    return rt_camera_render_region(cam, &r, rgb, radiance, stats);
+}
+
+int rt_camera_render_device(rt_camera* cam, const rt_launch* L, rt_render_stats* stats, uint64_t* work_counters) {
+    if (!cam || !L) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    try {
+        cam->ensure_device();
+        const hipStream_t stream = (hipStream_t)L->stream;
+        const int prec = L->precision < 0 ? cam->precision : L->precision;
+        cam->launch(L->region, L->tile_group, L->tile_groups, prec, L->count_work != 0, L->rgb, L->radiance,
+                    L->px_samples, L->px_bounces, stream);
+        if (L->synchronize) cam->read_stats(stats, L->count_work ? work_counters : nullptr, stream);
+        return RT_OK;
+    } catch (const HipError& e) {
+        return set_error(RT_ERR_DEVICE, e.what());
+    } catch (const std::invalid_argument& e) {
+        return set_error(RT_ERR_INVALID, e.what());
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_RENDER, e.what());
+    }
+}
+
+int rt_camera_export(const rt_camera* cam, void* nodes, void* prims, void* materials, void* lights,
+                     int32_t* prim_object) {
+    if (!cam) return set_error(RT_ERR_INVALID, "null camera");
+    const SceneBuild& b = cam->build;
+    if (nodes) std::memcpy(nodes, b.nodes.data(), b.nodes.size() * sizeof(RtNode));
+    if (prims) std::memcpy(prims, b.prims.data(), b.prims.size() * sizeof(RtPrim));
+    if (materials) std::memcpy(materials, b.mats.data(), b.mats.size() * sizeof(RtMat));
+    if (lights) std::memcpy(lights, b.lights.data(), b.lights.size() * sizeof(RtLight));
+    if (prim_object) std::memcpy(prim_object, b.prim_object.data(), b.prim_object.size() * sizeof(int32_t));
+    return RT_OK;
+}
+
+int rt_debug_world_hit(rt_camera* cam, int32_t n, const float* orig, const float* dir, double* out) {
+    if (!cam || n < 0 || (n > 0 && (!orig || !dir || !out))) return set_error(RT_ERR_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    float* d_o = nullptr;
+    float* d_d = nullptr;
+    double* d_out = nullptr;
+    try {
+        cam->ensure_device();
+        if (n == 0) return RT_OK;
+        hip_check(hipMalloc(&d_o, (size_t)n * 3 * sizeof(float)), "hipMalloc");
+        hip_check(hipMalloc(&d_d, (size_t)n * 3 * sizeof(float)), "hipMalloc");
+        hip_check(hipMalloc(&d_out, (size_t)n * 10 * sizeof(double)), "hipMalloc");
+        hip_check(hipMemcpy(d_o, orig, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
+        hip_check(hipMemcpy(d_d, dir, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
+        hip_check(launch_world_hit_ref(cam->dev_scene(), n, d_o, d_d, 0.001, INFINITY, d_out, nullptr),
+                  "world_hit_kernel");
+        hip_check(hipMemcpy(out, d_out, (size_t)n * 10 * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+        (void)hipFree(d_o);
+        (void)hipFree(d_d);
+        (void)hipFree(d_out);
+        return RT_OK;
+    } catch (const std::exception& e) {
+        if (d_o) (void)hipFree(d_o);
+        if (d_d) (void)hipFree(d_d);
+        if (d_out) (void)hipFree(d_out);
+        return set_error(RT_ERR_DEVICE, e.what());
+    }
+}
+
+int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out) {
+    if (n < 0 || (n > 0 && !out)) return set_error(RT_ERR_INVALID, "bad arguments");
+    uint64_t s = splitmix64((((uint64_t)pixel << 32) | sample) ^ splitmix64(seed));
+    for (int32_t k = 0; k < n; ++k) {
+        const uint64_t old = s;
+        s = old * 6364136223846793005ull + 1442695040888963407ull;
+        const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        const uint32_t rot = (uint32_t)(old >> 59u);
+        out[k] = (xs >> rot) | (xs << ((32u - rot) & 31u));
+    }
+    return RT_OK;
+}
+
+int rt_device_count(int32_t* count) {
+    if (!count) return set_error(RT_ERR_INVALID, "null argument");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RT_OK;
+}
+
+}  // extern "C"

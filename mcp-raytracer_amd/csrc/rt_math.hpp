@@ -1,0 +1,120 @@
+// JS-number / gl-matrix arithmetic model shared by the host scene builder and the
+// device path tracer.
+//
+// The reference stores every Vec3 in a gl-matrix Float32Array
+// (src/geometry/vec3.ts:3,19-25) while every scalar is a JS double. So a vector
+// op is "compute in double, round each component to fp32 on store", and a
+// scalar op is plain IEEE double. `Real` is the scalar type: `double` restates
+// the reference exactly ("ref" precision), `float` is the fast fp32 mode where
+// the round-to-fp32 steps become no-ops.
+//
+// Identities used to keep the ref mode cheap without changing a single bit:
+//  * a+b, a-b, a*b of two fp32 values computed in double and rounded to fp32
+//    equals the fp32 operation (double has > 2*24+2 bits), so vec+vec, vec-vec
+//    and vec*vec (gl-matrix add/subtract/multiply) are done directly in fp32.
+//  * products of two fp32 values are exact in double, so dot products only
+//    round in the two additions, exactly like `a[0]*b[0] + a[1]*b[1] + a[2]*b[2]`.
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#define RT_HD inline
+#endif
+
+namespace rt {
+
+using std::sqrt;
+
+struct V3 {
+    float x, y, z;
+};
+
+RT_HD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+
+// Vec3.create(x, y, z) with JS-number arguments: round each to fp32.
+template <class Real>
+RT_HD V3 mk(Real x, Real y, Real z) { return V3{(float)x, (float)y, (float)z}; }
+
+// gl-matrix vec3.add / subtract / multiply (component-wise): exact as fp32 ops.
+RT_HD V3 add(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RT_HD V3 sub(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RT_HD V3 mulv(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+
+// Vec3.multiply(t) = vec3.scale(out, a, t): double product, fp32 store.
+template <class Real>
+RT_HD V3 scale(V3 a, Real t) {
+    return V3{(float)((Real)a.x * t), (float)((Real)a.y * t), (float)((Real)a.z * t)};
+}
+// Vec3.divide(t) = vec3.scale(out, a, 1/t) (src/geometry/vec3.ts:126-130).
+template <class Real>
+RT_HD V3 divs(V3 a, Real t) { return scale<Real>(a, (Real)1 / t); }
+
+// Vec3.dot / lengthSquared (src/geometry/vec3.ts:132-136,152-157).
+template <class Real>
+RT_HD Real dot(V3 a, V3 b) {
+    return (Real)a.x * (Real)b.x + (Real)a.y * (Real)b.y + (Real)a.z * (Real)b.z;
+}
+template <class Real>
+RT_HD Real len2(V3 a) { return dot<Real>(a, a); }
+
+// gl-matrix vec3.cross: each component formed in double, rounded to fp32.
+template <class Real>
+RT_HD V3 cross(V3 a, V3 b) {
+    return V3{(float)((Real)a.y * (Real)b.z - (Real)a.z * (Real)b.y),
+              (float)((Real)a.z * (Real)b.x - (Real)a.x * (Real)b.z),
+              (float)((Real)a.x * (Real)b.y - (Real)a.y * (Real)b.x)};
+}
+
+// gl-matrix 3.4.3 vec3.normalize: len = x²+y²+z²; if (len > 0) len = 1/sqrt(len).
+template <class Real>
+RT_HD V3 unit(V3 a) {
+    Real l = (Real)a.x * (Real)a.x + (Real)a.y * (Real)a.y + (Real)a.z * (Real)a.z;
+    if (l > (Real)0) l = (Real)1 / sqrt(l);
+    return V3{(float)((Real)a.x * l), (float)((Real)a.y * l), (float)((Real)a.z * l)};
+}
+
+// Vec3.negate (src/geometry/vec3.ts:60-70): negation that normalises -0 to +0.
+RT_HD V3 neg(V3 a) {
+    V3 r{-a.x, -a.y, -a.z};
+    if (r.x == 0.0f) r.x = 0.0f;
+    if (r.y == 0.0f) r.y = 0.0f;
+    if (r.z == 0.0f) r.z = 0.0f;
+    return r;
+}
+
+// Vec3.reflect (src/geometry/vec3.ts:174-185): v - n*(2*(v·n)).
+template <class Real>
+RT_HD V3 reflect(V3 v, V3 n) {
+    Real d = dot<Real>(v, n);
+    return sub(v, scale<Real>(n, (Real)2 * d));
+}
+
+// JS Math.min / Math.max of two numbers: NaN-propagating, -0 < +0.
+template <class Real>
+RT_HD Real js_min(Real a, Real b) {
+    if (a != a || b != b) return a + b;  // NaN
+    if (a < b) return a;
+    if (b < a) return b;
+    return (a == (Real)0 && b == (Real)0) ? (__builtin_signbit(a) ? a : b) : a;
+}
+template <class Real>
+RT_HD Real js_max(Real a, Real b) {
+    if (a != a || b != b) return a + b;
+    if (a > b) return a;
+    if (b > a) return b;
+    return (a == (Real)0 && b == (Real)0) ? (__builtin_signbit(a) ? b : a) : a;
+}
+
+// Ray.at(t) = origin.add(direction.multiply(t)) (src/geometry/ray.ts:25-28).
+template <class Real>
+RT_HD V3 ray_at(V3 o, V3 d, Real t) { return add(o, scale<Real>(d, t)); }
+
+// Color.illuminance (src/geometry/vec3.ts:239-242), always a JS double.
+RT_HD double illuminance(V3 c) { return 0.299 * (double)c.x + 0.587 * (double)c.y + 0.114 * (double)c.z; }
+
+}  // namespace rt

@@ -1,0 +1,150 @@
+// Flattened, device-resident form of the reference's Camera + world.
+//
+// The reference builds an object graph per render (createCameraFromSceneData,
+// src/scenes/scenes.ts:60-104): Sphere/Plane/Quad objects (src/entities/*),
+// Material objects (src/materials/*), a recursive BVHNode tree
+// (src/geometry/bvh.ts:34-102) and a Camera (src/camera.ts:107-166). Here the
+// same data is laid out as flat arrays that one HIP kernel reads:
+//
+//   RtNode  32 B  BVH node in depth-first order, box + (left,right) or leaf range
+//   RtPrim  96 B  sphere / quad / plane, in leaf order, with its precomputed
+//                 plane frame (normal, D, w) exactly as Plane's constructor does
+//   RtMat   64 B  material table, nested materials by index, precomputed emission
+//   RtLight 16 B  light list (prim index + quad area), in object order
+//   RtCamera      frame vectors + render options
+//
+// Every fp32 field is produced by the same fp64-compute / fp32-store sequence
+// the reference runs, so the device sees bit-identical inputs.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "json.hpp"
+#include "rt_math.hpp"
+
+namespace rt {
+
+enum PrimType : int32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_PLANE = 2 };
+enum MatType : int32_t {
+    MAT_LAMBERT = 0,
+    MAT_METAL = 1,
+    MAT_GLASS = 2,
+    MAT_LIGHT = 3,
+    MAT_MIXED = 4,
+    MAT_LAYERED = 5,
+};
+enum RenderMode : int32_t { MODE_DEFAULT = 0, MODE_BOUNCES = 1, MODE_SAMPLES = 2 };
+
+struct alignas(16) RtNode {
+    float bmin[3];
+    int32_t a;  // interior: left child node; leaf: first prim
+    float bmax[3];
+    int32_t b;  // interior: right child node (>= 0); leaf: -count (< 0)
+};
+static_assert(sizeof(RtNode) == 32, "RtNode must be 32 bytes");
+
+struct alignas(16) RtPrim {
+    int32_t type;
+    int32_t mat;
+    double s0;     // sphere: radius (JS double); quad/plane: D = normal·Q (double)
+    float g0[4];   // sphere: center.xyz, (float)radius | quad/plane: Q.xyz, (float)D
+    float g1[4];   // quad/plane: u.xyz, -
+    float g2[4];   // quad/plane: v.xyz, -
+    float g3[4];   // quad/plane: normal.xyz, -
+    float g4[4];   // quad/plane: w.xyz, -
+};
+static_assert(sizeof(RtPrim) == 96, "RtPrim must be 96 bytes");
+
+struct alignas(16) RtMat {
+    int32_t type;
+    int32_t c0;      // mixed: material1 | layered: outer dielectric
+    int32_t c1;      // mixed: material2 | layered: inner
+    int32_t pad0;
+    float color[4];    // lambert/metal albedo, light emit
+    float emitted[4];  // Material.emitted(rec) (constant per material), fp32
+    double p0;         // metal: clamped fuzz | glass: ior | mixed: clamped weight
+    double pad1;
+};
+static_assert(sizeof(RtMat) == 64, "RtMat must be 64 bytes");
+
+struct alignas(16) RtLight {
+    int32_t prim;
+    int32_t type;
+    double area;  // quad: |u x v| via Math.hypot (double); sphere: unused
+};
+static_assert(sizeof(RtLight) == 16, "RtLight must be 16 bytes");
+
+struct RtCamera {
+    float pixel00[4];
+    float du[4];
+    float dv[4];
+    float center[4];
+    float ddu[4];  // defocusDiskU
+    float ddv[4];  // defocusDiskV
+    float bg_top[4];
+    float bg_bottom[4];
+    double aperture;
+    double samples;       // RenderOptions.samples (JS number)
+    double a_tolerance;
+    double a_batch;
+    double depth_raw;     // RenderOptions.depth as given (RenderMode.Bounces normalisation)
+    int32_t width;
+    int32_t height;
+    int32_t n_samples;    // loop count implied by `samples` (ceil, >= 0)
+    int32_t depth;        // bounces >= depth <=> bounces >= this (ceil of JS depth)
+    int32_t roulette;     // truthiness of RenderOptions.roulette
+    int32_t roulette_depth;
+    int32_t mode;         // RenderMode
+    int32_t adaptive;     // useAdaptiveSampling (src/camera.ts:165)
+    int32_t n_lights;
+    int32_t has_background;
+    int32_t emissive_scatter;  // some scattering material also emits (needs the emission stack)
+    int32_t n_nodes;
+    int32_t n_prims;
+    int32_t n_mats;
+    uint32_t seed;
+    int32_t stack_depth;  // BVH traversal stack entries needed (tree depth + 1)
+};
+
+// Per-launch render request (the reference's RenderRegion plus the build's RNG seed
+// and multi-GPU tile interleave). Tiles are 8x8 pixel blocks enumerated row-major
+// inside the region; this launch renders tiles t with t % tile_groups == tile_group.
+struct RtRegion {
+    int32_t x, y, width, height;
+    int32_t tile_group, tile_groups;
+};
+
+// Host-side build product. Owned by rt_camera; uploaded to the device lazily.
+struct SceneBuild {
+    std::vector<RtNode> nodes;
+    std::vector<RtPrim> prims;
+    std::vector<RtMat> mats;
+    std::vector<RtLight> lights;
+    RtCamera cam{};
+    int bvh_depth = 0;
+    std::vector<int32_t> prim_object;  // prim slot -> index in SceneData.objects
+};
+
+// createCameraFromSceneData(sceneData, renderOptions) restated
+// (src/scenes/scenes.ts:60-104). Throws std::runtime_error with the reference's
+// error message where the reference throws.
+SceneBuild build_scene(const rtj::Value& scene_data, const rtj::Value* render_options);
+
+// Scene generators (src/scenes/scenes-*.ts). `type` in {default, spheres, rain,
+// cornell}; options as the reference's *SceneOptions object (may be null).
+rtj::Value generate_scene_data(const std::string& type, const rtj::Value* options);
+
+// Math.hypot as implemented by V8 (Kahan-summed, max-normalised).
+double v8_hypot3(double x, double y, double z);
+
+// mulberry32 SeededRandom.next() with JS double seed arithmetic
+// (src/scenes/scenes-utils.ts:8-23).
+struct SeededRandom {
+    double seed;
+    explicit SeededRandom(double s) : seed(s) {}
+    double next();
+};
+
+}  // namespace rt

@@ -1,0 +1,77 @@
+"""Builds librt_amd.so (HIP kernels for gfx950 + the C ABI) in-tree.
+
+Plain hipcc invocations, no cmake: every source is compiled for
+--offload-arch=gfx950. The ref-precision kernel TU is compiled with
+-ffp-contract=off so no multiply-add is fused (the reference's JS arithmetic
+never fuses); the fp32 fast-mode TU may fuse.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+CSRC = PKG_DIR.parent / "csrc"
+INCLUDE = PKG_DIR.parent.parent / "include"
+LIB_DIR = PKG_DIR / "lib"
+LIB_PATH = LIB_DIR / "librt_amd.so"
+OBJ_DIR = PKG_DIR.parent / "build"
+
+ARCH = "gfx950"
+
+_COMMON = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+           f"-I{CSRC}", f"-I{INCLUDE}"]
+
+# (source, extra flags, is_hip)
+_UNITS = [
+    ("pt_ref.hip", ["-ffp-contract=off"], True),
+    ("pt_fp32.hip", ["-ffp-contract=fast"], True),
+    ("rt_api.cpp", ["-ffp-contract=off", "-x", "hip"], True),
+    ("scene.cpp", ["-ffp-contract=off"], False),
+]
+_HEADERS = ["json.hpp", "rt_math.hpp", "scene.hpp", "pt_kernel.hpp", "launch.hpp"]
+
+
+def hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP toolchain is required to build librt_amd.so")
+
+
+def _newest_input() -> float:
+    paths = [CSRC / u[0] for u in _UNITS] + [CSRC / h for h in _HEADERS] + [INCLUDE / "rt_amd.h", Path(__file__)]
+    return max(p.stat().st_mtime for p in paths)
+
+
+def build_native(force: bool = False, verbose: bool = False) -> Path:
+    """Compile (if stale) and return the path of librt_amd.so."""
+    if not force and LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= _newest_input():
+        return LIB_PATH
+    cc = hipcc()
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    objs = []
+    for src, flags, is_hip in _UNITS:
+        obj = OBJ_DIR / (src.replace(".", "_") + ".o")
+        cmd = [cc, *_COMMON, *flags]
+        if is_hip:
+            cmd.append(f"--offload-arch={ARCH}")
+        cmd += ["-c", str(CSRC / src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(str(obj))
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *objs]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build_native(force=True, verbose=True))

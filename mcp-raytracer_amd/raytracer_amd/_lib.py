@@ -1,0 +1,128 @@
+"""ctypes binding of librt_amd.so (include/rt_amd.h).
+
+The library is loaded from this package's lib/ directory only; if it is
+missing or does not export the ABI, import fails loudly - there is no CPU
+fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from pathlib import Path
+
+from ._build import LIB_PATH
+
+# Public header, parsed by tests to check that every declared symbol is exported.
+HEADER = Path(__file__).resolve().parents[2] / "include" / "rt_amd.h"
+
+RT_OK, RT_ERR_INVALID, RT_ERR_DEVICE, RT_ERR_RENDER = 0, 1, 2, 3
+PRECISION = {"ref": 0, "fp32": 1}
+
+CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_sphere",
+            "bounces", "diffuse", "samples", "rays"]
+
+
+class RtRegion(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class RtRenderStats(C.Structure):
+    _fields_ = [("pixels", C.c_double),
+                ("samples_total", C.c_double), ("samples_min", C.c_double),
+                ("samples_max", C.c_double), ("samples_avg", C.c_double),
+                ("bounces_total", C.c_double), ("bounces_min", C.c_double),
+                ("bounces_max", C.c_double), ("bounces_avg", C.c_double)]
+
+
+class RtCameraInfo(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("channels", C.c_int32),
+                ("n_objects", C.c_int32), ("n_nodes", C.c_int32), ("n_lights", C.c_int32),
+                ("n_materials", C.c_int32), ("bvh_depth", C.c_int32),
+                ("samples_loop", C.c_int32), ("depth", C.c_int32), ("roulette", C.c_int32),
+                ("roulette_depth", C.c_int32), ("mode", C.c_int32), ("adaptive", C.c_int32),
+                ("precision", C.c_int32), ("seed", C.c_uint32),
+                ("samples", C.c_double), ("aperture", C.c_double),
+                ("a_tolerance", C.c_double), ("a_batch", C.c_double)]
+
+
+class RtLaunch(C.Structure):
+    _fields_ = [("region", RtRegion), ("tile_group", C.c_int32), ("tile_groups", C.c_int32),
+                ("precision", C.c_int32), ("count_work", C.c_int32),
+                ("rgb", C.c_void_p), ("radiance", C.c_void_p),
+                ("px_samples", C.c_void_p), ("px_bounces", C.c_void_p),
+                ("stream", C.c_void_p), ("synchronize", C.c_int32)]
+
+
+class RtError(RuntimeError):
+    """An error returned through the C ABI (the reference would throw an Error)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+_SIGS = {
+    "rt_version": (C.c_int, []),
+    "rt_last_error": (C.c_char_p, []),
+    "rt_free": (None, [C.c_void_p]),
+    "rt_generate_scene_data": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "rt_camera_create": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "rt_camera_destroy": (None, [C.c_void_p]),
+    "rt_camera_get_info": (C.c_int, [C.c_void_p, C.POINTER(RtCameraInfo)]),
+    "rt_camera_set_precision": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rt_camera_render_region": (C.c_int, [C.c_void_p, C.POINTER(RtRegion), C.c_void_p, C.c_void_p,
+                                          C.POINTER(RtRenderStats)]),
+    "rt_camera_render": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(RtRenderStats)]),
+    "rt_camera_render_device": (C.c_int, [C.c_void_p, C.POINTER(RtLaunch), C.POINTER(RtRenderStats),
+                                          C.POINTER(C.c_uint64)]),
+    "rt_camera_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p]),
+    "rt_debug_world_hit": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_void_p]),
+    "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load librt_amd.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"librt_amd.so not found at {LIB_PATH}; run __graft_entry__.build() "
+                          "(hipcc --offload-arch=gfx950) first - there is no CPU fallback")
+    # PyTorch-ROCm ships its own libamdhip64.so.7 (same soname as /opt/rocm's).
+    # Whichever loads first serves the whole process, and torch cannot run on a
+    # newer runtime, so let torch's copy load first when torch is installed; the
+    # library then shares torch's HIP runtime (device memory, streams).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = C.CDLL(os.fspath(LIB_PATH))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(code: int) -> None:
+    if code != RT_OK:
+        msg = load().rt_last_error()
+        raise RtError(code, msg.decode("utf-8", "replace") if msg else f"rt error {code}")
+
+
+def to_json(obj) -> bytes:
+    """Serialise like JSON.stringify, keeping Infinity/NaN (accepted by the C parser)."""
+    return json.dumps(obj, allow_nan=True, separators=(",", ":")).encode()
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    check(load().rt_device_count(C.byref(n)))
+    return int(n.value)
