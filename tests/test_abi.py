@@ -1,0 +1,110 @@
+"""The C ABI boundary (include/rt_amd.h): exports, host-side behaviour and the
+reference's error behaviour. No GPU needed (no render calls)."""
+import ctypes
+import re
+
+import pytest
+
+
+def test_library_exports_every_declared_symbol(rt):
+    from raytracer_amd import _lib
+    lib = _lib.load()
+    text = _lib.HEADER.read_text()
+    names = set(re.findall(r"^\s*(?:int|void|const char\*)\s+\**(rt_\w+)\s*\(", text, re.M))
+    assert len(names) >= 14
+    for n in sorted(names):
+        assert hasattr(lib, n), f"{n} declared in rt_amd.h but not exported"
+    assert lib.rt_version() == 1
+
+
+def test_library_is_gfx950_code_object(rt):
+    from raytracer_amd import _lib
+    data = _lib.LIB_PATH.read_bytes()
+    assert b"gfx950" in data
+    assert b"pt_render_kernel" in data
+
+
+def test_camera_info_defaults_and_merge_order(rt):
+    sd = rt.generate_scene_data({"type": "cornell"})
+    cam = rt.create_camera_from_scene_data(sd)  # render defaults + scene render {aspect 1, rouletteDepth 5}
+    i = cam.info
+    assert (i["width"], i["height"]) == (400, 400)
+    assert i["samples"] == 100 and i["depth"] == 100 and i["roulette_depth"] == 5 and i["adaptive"] == 1
+    assert i["a_tolerance"] == 0.05 and i["a_batch"] == 10
+    # provided render options win over the scene's (scenes.ts:97-100)
+    cam = rt.create_camera_from_scene_data(sd, {"width": 50, "aspect": 2, "rouletteDepth": 2, "aTolerance": 0})
+    i = cam.info
+    assert (i["width"], i["height"], i["roulette_depth"], i["adaptive"]) == (50, 25, 2, 0)
+    d = rt.create_camera_from_scene_data(rt.generate_scene_data({"type": "rain", "options": {"seed": 1}}))
+    assert (d.image_width, d.image_height) == (400, 225)  # 16:9 default (camera.test.ts:161-166)
+
+
+def test_precision_option(rt):
+    sd = rt.generate_scene_data({"type": "cornell"})
+    assert rt.create_camera_from_scene_data(sd).precision == "ref"
+    assert rt.create_camera_from_scene_data(sd, {"precision": "fp32"}).precision == "fp32"
+    with pytest.raises(rt.RtError):
+        rt.create_camera_from_scene_data(sd, {"precision": "half"})
+
+
+@pytest.mark.parametrize("mutate,msg", [
+    (lambda s: s["objects"][0].__setitem__("material", "nope"), "Material not found: nope"),
+    (lambda s: s["objects"][0].__setitem__("type", "cone"), "Unknown object type: cone"),
+    (lambda s: s["materials"][0]["material"].__setitem__("type", "plastic"), "Unknown material type: plastic"),
+    (lambda s: s.__setitem__("objects", []), "reading 'maximum'"),
+    (lambda s: s["objects"][0].__setitem__("material", {"type": "layered", "outer": {"type": "lambert",
+                                                        "color": [1, 1, 1]}, "inner": "red"}),
+     "Material is not a dielectric"),
+])
+def test_reference_errors(rt, mutate, msg):
+    sd = rt.generate_scene_data({"type": "cornell"})
+    mutate(sd)
+    with pytest.raises(rt.RtError, match=re.escape(msg)):
+        rt.create_camera_from_scene_data(sd)
+
+
+def test_missing_vfov_gives_nan_camera_not_error(rt):
+    """{...defaults, ...{vfov: undefined}} overrides the default with undefined
+    (scenes.ts:83-94 -> camera.ts:115): the camera is built, its frame is NaN."""
+    sd = rt.generate_scene_data({"type": "cornell"})
+    del sd["camera"]["vfov"]
+    cam = rt.create_camera_from_scene_data(sd, {"width": 8})
+    assert cam.image_width == 8
+
+
+def test_unknown_scene_type(rt):
+    with pytest.raises(rt.RtError):
+        rt.generate_scene_data({"type": "teapot"})
+
+
+def test_metal_fuzz_and_mixed_weight_clamps(rt):
+    sd = {"camera": {"vfov": 40, "from": [0, 0, 1], "at": [0, 0, 0], "up": [0, 1, 0],
+                     "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [1, 1, 1]}},
+          "objects": [
+              {"type": "sphere", "pos": [0, 0, 0], "r": 1, "material": {"type": "metal", "color": [1, 1, 1],
+                                                                         "fuzz": 3}},
+              {"type": "sphere", "pos": [0, 0, 0], "r": 1, "material": {"type": "metal", "color": [1, 1, 1]}},
+              {"type": "sphere", "pos": [0, 0, 0], "r": 1, "material": {"type": "mixed", "weight": -2,
+                                                                         "diff": {"type": "lambert", "color": [1, 1, 1]},
+                                                                         "spec": {"type": "light", "emit": [2, 2, 2]}}},
+          ]}
+    mats = rt.create_camera_from_scene_data(sd, {"width": 4}).export()["materials"]
+    metals = mats[mats["type"] == 1]
+    assert sorted(metals["p0"].tolist()) == [0.0, 1.0]  # fuzz 3 -> 1; missing -> 0
+    mixed = mats[mats["type"] == 4]
+    assert mixed["p0"][0] == 0.0  # weight clamped into [0, 1]
+    assert list(mixed["emitted"][0][:3]) == [2.0, 2.0, 2.0]  # E1*0 + E2*(1-0)
+
+
+def test_png_encoder_roundtrip():
+    from raytracer_amd.png import decode_png_rgb, encode_png
+    import numpy as np
+    px = (np.arange(5 * 3 * 3) % 251).astype(np.uint8)
+    w, h, out = decode_png_rgb(encode_png(px.tobytes(), 5, 3))
+    assert (w, h) == (5, 3) and out == px.tobytes()
+
+
+def test_divide_into_regions_matches_reference(rt):
+    regs = rt.divide_into_regions(10, 7, 3)
+    assert [(r["y"], r["height"]) for r in regs] == [(0, 3), (3, 3), (6, 1)]
+    assert len(rt.divide_into_regions(10, 2, 8)) == 2

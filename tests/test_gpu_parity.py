@@ -156,6 +156,15 @@ def test_tile_groups_partition_the_image(rt, gpu):
     torch.cuda.synchronize()
     assert total == W * H
     assert torch.equal(acc, full)
+    # the kernel's tile walk is exactly raytracer_amd.distributed.owner_mask
+    from raytracer_amd.distributed import owner_mask
+    for g in range(3):
+        pxs = torch.full((H, W), -1, dtype=torch.int32, device="cuda")
+        part = torch.zeros_like(full)
+        cam.render_device(rgb_ptr=part.data_ptr(), px_samples_ptr=pxs.data_ptr(), tile_group=g, tile_groups=3,
+                          synchronize=True)
+        written = (pxs >= 0).cpu().numpy()
+        assert np.array_equal(written, owner_mask(W, H, (0, 0, W, H), g, 3))
 
 
 def test_fp32_precision_within_tolerance(rt, oracle, gpu):

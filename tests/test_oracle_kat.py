@@ -1,0 +1,203 @@
+"""Pin the oracle's building blocks to the reference's own known-answer tests.
+
+Each case cites the jest test it transcribes (paths under the reference's
+tests/). jest's toBeCloseTo(x) default precision 2 means |d| < 0.005;
+toBeCloseTo(x, p) means |d| < 10**-p / 2.
+"""
+import math
+
+import pytest
+
+
+def close(a, b, p=2):
+    return abs(a - b) < 10 ** (-p) / 2
+
+
+# ---- tests/entities/sphere.test.ts:16-90 -----------------------------------
+def test_sphere_hit_kats(oracle):
+    c, r = (0, 0, -1), 0.5
+    h = oracle.sphere_hit(c, r, (0, 0, 0), (0, 0, -1), 0, math.inf)
+    assert h["hit"] and close(h["t"], 0.5)
+    assert all(close(a, b) for a, b in zip(h["p"], (0, 0, -0.5)))
+    assert all(close(a, b) for a, b in zip(h["normal"], (0, 0, 1)))  # outward
+    assert h["front"] is True
+    assert not oracle.sphere_hit(c, r, (0, 1, 0), (0, 0, -1), 0, math.inf)["hit"]
+    h = oracle.sphere_hit(c, r, (0, 0, -1), (0, 0, -1), 0.001, math.inf)  # from inside
+    assert h["hit"] and close(h["t"], 0.5) and all(close(a, b) for a, b in zip(h["p"], (0, 0, -1.5)))
+    assert all(close(a, b) for a, b in zip(h["normal"], (0, 0, 1)))  # -(outward (0,0,-1))
+    assert h["front"] is False
+    h = oracle.sphere_hit(c, r, (0, 0.5, 0), (0, 0, -1), 0, math.inf)  # grazing
+    assert h["hit"] and close(h["t"], 1.0) and h["front"] is True
+    assert not oracle.sphere_hit(c, r, (0, 0, 0), (0, 0, -1), 0.6, 1.0)["hit"]
+    assert not oracle.sphere_hit(c, r, (0, 0, 0), (0, 0, -1), 0.0, 0.4)["hit"]
+
+
+# ---- tests/entities/sphere.test.ts:99-152 ----------------------------------
+def test_sphere_pdf_kats(oracle):
+    c, r = (0, 0, -1), 0.5
+    assert oracle.sphere_pdf_value(c, r, (0, 0, 0), (0, 1, 0)) == 0
+    v = oracle.sphere_pdf_value(c, r, (0, 0, 0), (0, 0, -1))
+    expected = 1 / (2 * math.pi * (1 - math.sqrt(1 - 0.25)))
+    assert close(v, expected, 5)
+    assert oracle.sphere_pdf_value(c, r, (0, 0, 5), (0, 0, -1)) > v
+
+
+# ---- tests/entities/quad.test.ts:17-203,240-261 ----------------------------
+def test_quad_kats(oracle):
+    assert close(oracle.quad_area((1, 0, 0), (0, 1, 0)), 1)
+    assert close(oracle.quad_area((2, 0, 0), (0, 3, 0)), 6)
+    q, u, v = (0, 0, 5), (1, 0, 0), (0, 1, 0)
+    h = oracle.quad_hit(q, u, v, (0.5, 0.5, 0), (0, 0, 1), 0, math.inf)
+    assert h["hit"] and close(h["t"], 5) and all(close(a, b) for a, b in zip(h["p"], (0.5, 0.5, 5)))
+    assert not oracle.quad_hit(q, u, v, (1.5, 0.5, 0), (0, 0, 1), 0, math.inf)["hit"]
+    for corner in [(0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0)]:  # corners are inclusive
+        h = oracle.quad_hit(q, u, v, corner, (0, 0, 1), 0, math.inf)
+        assert h["hit"] and close(h["t"], 5)
+    assert not oracle.quad_hit(q, u, v, (0, 0, 0), (1, 1, 0), 0, math.inf)["hit"]  # parallel
+    f = oracle.quad_hit(q, u, v, (0.5, 0.5, 0), (0, 0, 1), 0, math.inf)
+    assert f["front"] is False and close(f["normal"][2], -1)
+    b = oracle.quad_hit(q, u, v, (0.5, 0.5, 10), (0, 0, -1), 0, math.inf)
+    assert b["front"] is True and close(b["normal"][2], 1)
+    mn, mx = oracle.prim_box("quad", (1, 2, 5), (3, 0, 0), (0, 4, 0))
+    for a, e in zip(mn + mx, [1 - 1e-4, 2 - 1e-4, 5 - 1e-4, 4 + 1e-4, 6 + 1e-4, 5 + 1e-4]):
+        assert close(a, e)
+    mn, mx = oracle.prim_box("quad", (0, 0, 0), (1, 1, 0), (0, 1, 1))
+    for a, e in zip(mn + mx, [-1e-4, -1e-4, -1e-4, 1 + 1e-4, 2 + 1e-4, 1 + 1e-4]):
+        assert close(a, e)
+    # pdfValue: miss -> 0; hit -> dist^2 / (area * |cos|)
+    assert oracle.quad_pdf_value(q, u, v, (0, 0, 0), (0, 1, 0)) == 0
+    d = oracle.unit((0.5, 0.5, 5))
+    pv = oracle.quad_pdf_value(q, u, v, (0, 0, 0), d)
+    dist2 = 0.5 ** 2 + 0.5 ** 2 + 25
+    expected = dist2 / (1 * abs(d[2]))
+    assert pv > 0 and close(pv, expected, 5 - 3)  # fp32-stored direction: compare to 1e-3 relative scale
+    assert abs(pv - expected) / expected < 1e-6
+
+
+# ---- tests/entities/quad.test.ts:356-370 (just outside the edge) ----------
+def test_quad_barely_misses(oracle):
+    assert not oracle.quad_hit((0, 0, 5), (1, 0, 0), (0, 1, 0), (1.0001, 0.5, 0), (0, 0, 1), 0, math.inf)["hit"]
+
+
+# ---- tests/entities/plane.test.ts:100-136,211-287 --------------------------
+def test_plane_kats(oracle):
+    r = oracle.plane_intersect((0, 0, 0), (2, 0, 0), (0, 3, 0), (1, 1.5, -1), (0, 0, 1), 0, math.inf)
+    assert r["hit"] and close(r["t"], 1) and close(r["alpha"], 0.5) and close(r["beta"], 0.5)
+    assert not oracle.plane_intersect((0, 0, 5), (1, 0, 0), (0, 1, 0), (0, 0, 0), (0, 0, 1), 0, 4)["hit"]
+    inf = math.inf
+    mn, mx = oracle.prim_box("plane", (0, 0, 5), (1, 0, 0), (0, 1, 0))
+    assert mn[:2] == [-inf, -inf] and mx[:2] == [inf, inf] and close(mn[2], 5 - 1e-4) and close(mx[2], 5 + 1e-4)
+    mn, mx = oracle.prim_box("plane", (0, 3, 0), (1, 0, 0), (0, 0, 1))
+    assert mn[0] == -inf and mn[2] == -inf and close(mn[1], 3 - 1e-4) and close(mx[1], 3 + 1e-4)
+    mn, mx = oracle.prim_box("plane", (-2, 0, 0), (0, 1, 0), (0, 0, 1))
+    assert close(mn[0], -2 - 1e-4) and close(mx[0], -2 + 1e-4) and mn[1] == -inf and mx[2] == inf
+    mn, mx = oracle.prim_box("plane", (0, 0, 0), (1, 1, 0), (0, 1, 1))
+    assert mn == [-inf] * 3 and mx == [inf] * 3
+
+
+# ---- tests/geometry/aabb.test.ts:6-66 --------------------------------------
+def test_aabb_kats(oracle):
+    box = ((-1, -1, -1), (1, 1, 1))
+    assert oracle.aabb_hit(*box, (0, 0, -5), (0, 0, 1), 0.1, 100)
+    assert not oracle.aabb_hit(*box, (5, 0, 0), (0, 0, 1), 0.1, 100)
+    assert not oracle.aabb_hit(*box, (0, 0, -5), (0, 0, 1), 0.1, 3)
+
+
+def test_aabb_weak_per_axis_test_is_reference_behaviour(oracle):
+    """AABB.hit clips each axis against the ORIGINAL interval (aabb.ts:49-54),
+    so a ray that passes each slab at different times still 'hits'."""
+    # Ray along +x+y: x-slab at t in [4,6], y-slab at t in [-1,1] (the intervals don't overlap).
+    box = ((4, -1, -1), (6, 1, 1))
+    assert oracle.aabb_hit(*box, (0, 0, 0), (1, 1, 0.0001), 0.001, math.inf)
+
+
+# ---- tests/geometry/pdf.test.ts:55-77,126-156 ------------------------------
+def test_cosine_pdf_kats(oracle):
+    n = (0, 1, 0)
+    assert close(oracle.cosine_pdf_value(n, (0, 1, 0)), 1 / math.pi)
+    assert close(oracle.cosine_pdf_value(n, oracle.unit((1, 1, 0))), 0.7071 / math.pi, 4)
+    assert close(oracle.cosine_pdf_value(n, (1, 0, 0)), 0)
+    assert oracle.cosine_pdf_value(n, (0, -1, 0)) == 0
+
+
+def test_mixture_pdf_kats(oracle):
+    assert close(oracle.mixture_value([1, 1], [0.5, 0.5]), 1.0)
+    assert close(oracle.mixture_value([1, 3], [0.5, 0.5]), 2)
+    assert close(oracle.mixture_value([1, 3], [1, 3]), 2.5)
+
+
+# ---- tests/materials/dielectric.test.ts:109-135 ----------------------------
+def test_schlick_kats(oracle):
+    perp = oracle.schlick(1.0, 1 / 1.5)
+    graz = oracle.schlick(0.1, 1 / 1.5)
+    assert graz > perp
+    assert close(perp, 0.04, 1)
+    assert graz > 0.5
+
+
+# ---- tests/materials/metal.test.ts:30-73 -----------------------------------
+def test_metal_reflect_kat(oracle):
+    d = oracle.unit((1, -1, 0))
+    r = oracle.reflect(d, (0, 1, 0))
+    e = oracle.unit((1, 1, 0))
+    assert all(close(a, b, 5) for a, b in zip(r, e))
+
+
+# ---- tests/geometry/vec3.test.ts (gl-matrix boundary) ----------------------
+def test_vec3_boundary(oracle):
+    assert oracle.length((3, 4, 0)) == 5.0
+    assert oracle.unit((0, 0, 0)) == [0, 0, 0]  # len 0: normalize leaves zeros
+    u = oracle.unit((1, 2, 2))
+    assert all(close(a, b, 6) for a, b in zip(u, (1 / 3, 2 / 3, 2 / 3)))
+    # fp32 storage: components are exactly representable floats
+    import numpy as np
+    assert all(np.float32(a) == a for a in u)
+    r = oracle.refract((0, -1, 0), (0, 1, 0), 1 / 1.5)  # normal incidence passes straight through
+    assert all(close(a, b, 6) for a, b in zip(r, (0, -1, 0)))
+
+
+# ---- tests/camera.test.ts:161-174 (dimensions) -----------------------------
+def test_camera_dimensions(oracle):
+    scene = {"camera": {"vfov": 90, "from": [0, 0, 0], "at": [0, 0, -1], "up": [0, 1, 0],
+                        "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [0.5, 0.7, 1]}},
+             "objects": [{"type": "sphere", "pos": [0, 0, -1], "r": 0.5, "material": {"type": "lambert",
+                                                                                     "color": [0.5, 0.5, 0.5]}}]}
+    d = oracle.camera_info(scene)
+    assert (d["width"], d["height"]) == (400, 225)
+    d = oracle.camera_info(scene, {"width": 100, "aspect": 1.0})
+    assert (d["width"], d["height"]) == (100, 100)
+
+
+# ---- tests/camera.test.ts:725-816 (background lerp) ------------------------
+@pytest.mark.parametrize("look,expect", [((0, 1, 0), "bottom"), ((0, -1, 0), "top")])
+def test_background_gradient(oracle, look, expect):
+    top, bottom = [1.0, 0.0, 0.0], [0.0, 1.0, 0.0]
+    scene = {"camera": {"vfov": 1, "from": [0, 0, 0], "at": list(look), "up": [1, 0, 0], "focus": 1,
+                        "background": {"type": "gradient", "top": top, "bottom": bottom}},
+             "objects": [{"type": "sphere", "pos": [100, 100, 100], "r": 0.1,
+                          "material": {"type": "lambert", "color": [1, 1, 1]}}]}
+    out = oracle.render(scene, {"width": 4, "aspect": 1, "samples": 1, "aTolerance": 0})
+    c = out["radiance"][2, 2]
+    want = bottom if expect == "bottom" else top
+    assert all(close(a, b, 2) for a, b in zip(c, want))
+
+
+# ---- tests/camera.test.ts:331-396 (render stats) ---------------------------
+def test_render_stats_kats(oracle):
+    scene = {"camera": {"vfov": 90, "from": [0, 0, 0], "at": [0, 0, -1], "up": [0, 1, 0], "aperture": 0,
+                        "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [0.5, 0.7, 1]}},
+             "objects": [{"type": "sphere", "pos": [0, 0, -1], "r": 0.5, "material": {"type": "lambert",
+                                                                                     "color": [0.5, 0.5, 0.5]}}]}
+    out = oracle.render(scene, {"width": 10, "aspect": 1.0, "samples": 1})
+    st = out["stats"]
+    assert st["samples"]["total"] == 100 and st["pixels"] == 100
+    assert st["samples"]["min"] == 1 and st["samples"]["max"] == 1
+    assert st["bounces"]["min"] >= 0
+    out = oracle.render(scene, {"width": 20, "aspect": 1.0, "samples": 1}, region=(5, 5, 10, 10))
+    assert out["stats"]["pixels"] == 100 and out["stats"]["samples"]["total"] == 100
+
+
+def test_rng_stream_product_matches_oracle(oracle, rt):
+    """The seeded Math.random replacement: product (host) and oracle streams agree bit-for-bit."""
+    for key in [(0x5EED, 0, 0), (1, 12345, 7), (0xFFFFFFFF, 4096 * 4096 - 1, 1023)]:
+        assert rt.rng_stream(*key, 64) == oracle.rng_stream(*key, 64)
