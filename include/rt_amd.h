@@ -42,6 +42,11 @@ enum {
 };
 
 enum { RT_PRECISION_REF = 0, RT_PRECISION_FP32 = 1 };
+/* BVH traversal. Both return the reference's closest hit bit-for-bit:
+ * REFERENCE visits nodes in BVHNode.hit's order with AABB.hit's per-axis test
+ * (src/geometry/bvh.ts:128-146); FAST culls with a strict slab test on padded
+ * boxes, near child first, and breaks t ties by leaf order. */
+enum { RT_TRAVERSAL_FAST = 0, RT_TRAVERSAL_REFERENCE = 1 };
 
 typedef struct rt_camera rt_camera;
 
@@ -62,7 +67,7 @@ typedef struct {
 typedef struct {
     int32_t width, height, channels;
     int32_t n_objects, n_nodes, n_lights, n_materials, bvh_depth;
-    int32_t samples_loop, depth, roulette, roulette_depth, mode, adaptive, precision;
+    int32_t samples_loop, depth, roulette, roulette_depth, mode, adaptive, precision, traversal;
     uint32_t seed;
     double samples, aperture, a_tolerance, a_batch;
 } rt_camera_info;
@@ -76,6 +81,7 @@ typedef struct {
     rt_region region;
     int32_t tile_group, tile_groups;
     int32_t precision;       /* -1: the camera's precision */
+    int32_t traversal;       /* -1: the camera's; RT_TRAVERSAL_FAST / RT_TRAVERSAL_REFERENCE */
     int32_t count_work;      /* 1: instrumented build, fills work_counters */
     uint8_t* rgb;            /* device, may be NULL */
     float* radiance;         /* device, may be NULL */
@@ -126,9 +132,11 @@ int rt_camera_render_device(rt_camera* cam, const rt_launch* launch, rt_render_s
 int rt_camera_export(const rt_camera* cam, void* nodes, void* prims, void* materials, void* lights,
                      int32_t* prim_object);
 
-/* Closest hit of n rays through the device BVH (ref precision). orig/dir: host
- * float[3*n]; out: host double[10*n] = {hit, t, p.xyz, n.xyz, front, prim_slot}. */
-int rt_debug_world_hit(rt_camera* cam, int32_t n, const float* orig, const float* dir, double* out);
+/* Closest hit of n rays through the device BVH (ref precision; traversal -1 =
+ * the camera's). orig/dir: host float[3*n]; out: host double[10*n] =
+ * {hit, t, p.xyz, n.xyz, front, prim_slot}. */
+int rt_debug_world_hit(rt_camera* cam, int32_t traversal, int32_t n, const float* orig, const float* dir,
+                       double* out);
 
 /* The path RNG stream (seeded Math.random replacement), host evaluation. */
 int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out);

@@ -4,18 +4,22 @@
 
 namespace rt {
 
-template <bool EMIT, bool COUNT>
+template <bool EMIT, bool COUNT, bool FAST>
 static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                      hipStream_t stream) {
-    hipLaunchKernelGGL((pt_render_kernel<float, EMIT, COUNT>), dim3(g.grid), dim3(kBlock), g.lds_bytes, stream, S,
-                       reg, out, g.tiles_x, g.my_tiles);
+    hipLaunchKernelGGL((pt_render_kernel<float, EMIT, COUNT, FAST>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+                       stream, S, reg, out, g.tiles_x, g.my_tiles);
     return hipGetLastError();
 }
 
-hipError_t launch_render_fp32(bool emit, bool count, const DevScene& S, const RtRegion& reg, const RenderOut& out,
+hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
                               const LaunchGeom& g, hipStream_t stream) {
-    if (emit) return count ? go<true, true>(S, reg, out, g, stream) : go<true, false>(S, reg, out, g, stream);
-    return count ? go<false, true>(S, reg, out, g, stream) : go<false, false>(S, reg, out, g, stream);
+    if (v.fast) {
+        if (v.emit) return v.count ? go<true, true, true>(S, reg, out, g, stream) : go<true, false, true>(S, reg, out, g, stream);
+        return v.count ? go<false, true, true>(S, reg, out, g, stream) : go<false, false, true>(S, reg, out, g, stream);
+    }
+    if (v.emit) return v.count ? go<true, true, false>(S, reg, out, g, stream) : go<true, false, false>(S, reg, out, g, stream);
+    return v.count ? go<false, true, false>(S, reg, out, g, stream) : go<false, false, false>(S, reg, out, g, stream);
 }
 
 }  // namespace rt

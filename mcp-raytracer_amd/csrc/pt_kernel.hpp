@@ -33,7 +33,8 @@
 namespace rt {
 
 struct DevScene {
-    const RtNode* __restrict__ nodes;
+    const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
+    const RtNode* __restrict__ fnodes;  // same tree, boxes padded outward (fast traversal)
     const RtPrim* __restrict__ prims;
     const RtMat* __restrict__ mats;
     const RtLight* __restrict__ lights;
@@ -257,6 +258,190 @@ __device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& 
     return hit;
 }
 
+// ---------------------------------------------------------------------------
+// Fast traversal with the SAME result.
+//
+// The reference tests primitive k with the closest-so-far interval and keeps
+// it iff its first root t_k in (0.001, inf) satisfies t_k < tmax (strict), in
+// DFS leaf order. So its answer is the lexicographic minimum of (t_k, leaf
+// slot) over all primitives - independent of visiting order - provided no box
+// containing a valid hit is culled. This traversal therefore
+//   * culls with a strict fp32 slab test (the reference's per-axis test culls
+//     far less) on boxes padded outward by ~1e-6 relative, accepting ties,
+//   * visits the nearer child first and culls stacked nodes against the best t,
+//   * rejects a primitive from an fp32 estimate only when it is clearly not a
+//     candidate, and otherwise computes t_k with the reference's exact
+//     arithmetic (Real) and compares (t, slot) lexicographically.
+// The parity tests check it bit-for-bit against both the oracle and the
+// reference-order traversal above.
+// ---------------------------------------------------------------------------
+struct FRay {
+    float o[3];
+    float d[3];
+    float inv[3];  // 1/d with zero components replaced by +-1e-30 (no 0*inf NaNs)
+    float a;       // |d|^2
+};
+
+__device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
+    FRay f;
+    f.o[0] = o.x; f.o[1] = o.y; f.o[2] = o.z;
+    f.d[0] = d.x; f.d[1] = d.y; f.d[2] = d.z;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float c = f.d[a];
+        const float cc = ::fabsf(c) < 1e-30f ? ::copysignf(1e-30f, c) : c;
+        f.inv[a] = 1.0f / cc;
+    }
+    f.a = d.x * d.x + d.y * d.y + d.z * d.z;
+    return f;
+}
+
+constexpr float kTminLo = 0.001f * (1.0f - 1e-5f);
+
+__device__ __forceinline__ bool slab(const RtNode& n, const FRay& f, float thi, float& tnear) {
+    if (n.bmin[0] != n.bmin[0]) return false;  // box the reference can never enter
+    float tn = kTminLo, tf = thi;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float t0 = (n.bmin[a] - f.o[a]) * f.inv[a];
+        const float t1 = (n.bmax[a] - f.o[a]) * f.inv[a];
+        tn = ::fmaxf(tn, ::fminf(t0, t1));
+        tf = ::fminf(tf, ::fmaxf(t0, t1));
+    }
+    tnear = tn;
+    return tn <= tf * 1.000002f;
+}
+
+// fp32 pre-filters: false only when the exact test surely gives no t <= thi.
+__device__ __forceinline__ bool sphere_maybe(const RtPrim& p, const FRay& f, float thi) {
+    const float ox = f.o[0] - p.g0[0], oy = f.o[1] - p.g0[1], oz = f.o[2] - p.g0[2];
+    const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
+    const float r = p.g0[3];
+    const float c = (ox * ox + oy * oy + oz * oz) - r * r;
+    const float disc = b * b - f.a * c;
+    const float tol = 1e-4f * (b * b + ::fabsf(f.a * c)) + 1e-30f;
+    if (disc < -tol) return false;
+    const float sq = ::sqrtf(::fmaxf(disc, 0.0f) + tol);
+    const float et = 1e-4f * (::fabsf(b) + sq) / f.a;
+    if ((-b + sq) / f.a + et < kTminLo) return false;
+    if ((-b - sq) / f.a - et > thi) return false;
+    return true;
+}
+
+template <bool QUAD>
+__device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, float thi) {
+    const float nx = p.g3[0], ny = p.g3[1], nz = p.g3[2];
+    const float denom = nx * f.d[0] + ny * f.d[1] + nz * f.d[2];
+    if (!(::fabsf(denom) > 1e-6f * ::sqrtf(f.a))) return true;  // near-parallel: decide exactly
+    const float no = nx * f.o[0] + ny * f.o[1] + nz * f.o[2];
+    const float D = p.g0[3];
+    const float t = (D - no) / denom;
+    const float et = 1e-4f * (::fabsf(D) + ::fabsf(no)) / ::fabsf(denom) + 1e-30f;
+    if (t + et < kTminLo || t - et > thi) return false;
+    if (!QUAD) return true;
+    const float px = f.o[0] + t * f.d[0] - p.g0[0];
+    const float py = f.o[1] + t * f.d[1] - p.g0[1];
+    const float pz = f.o[2] + t * f.d[2] - p.g0[2];
+    const float ux = p.g1[0], uy = p.g1[1], uz = p.g1[2];
+    const float vx = p.g2[0], vy = p.g2[1], vz = p.g2[2];
+    const float wx = p.g4[0], wy = p.g4[1], wz = p.g4[2];
+    // alpha = w . (ph x v), beta = w . (u x ph)
+    const float alpha = wx * (py * vz - pz * vy) + wy * (pz * vx - px * vz) + wz * (px * vy - py * vx);
+    const float beta = wx * (uy * pz - uz * py) + wy * (uz * px - ux * pz) + wz * (ux * py - uy * px);
+    const float ea = 1e-3f;
+    if (alpha < -ea || alpha > 1.0f + ea || beta < -ea || beta > 1.0f + ea) return false;
+    return true;
+}
+
+// Exact candidate t (reference arithmetic) of primitive p on (0.001, inf).
+template <class Real, bool COUNT>
+__device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>& r, const FRay& f, float thi,
+                                               Real& t, uint32_t* cnt) {
+    const Real inf = (Real)__builtin_inf();
+    if (p.type == PRIM_SPHERE) {
+        if (COUNT) cnt[CT_SPHERE]++;
+        if (!sphere_maybe(p, f, thi)) return false;
+        return sphere_t<Real>(p, r, K<Real>::TMIN, inf, t);
+    }
+    if (p.type == PRIM_QUAD) {
+        if (COUNT) cnt[CT_QUAD]++;
+        if (!planar_maybe<true>(p, f, thi)) return false;
+        return planar_t<Real, true>(p, r, K<Real>::TMIN, inf, t);
+    }
+    if (COUNT) cnt[CT_PLANE]++;
+    if (!planar_maybe<false>(p, f, thi)) return false;
+    return planar_t<Real, false>(p, r, K<Real>::TMIN, inf, t);
+}
+
+template <class Real>
+__device__ __forceinline__ float upper_f(Real t) {
+    // fp32 value >= t (rounded up with margin) used to cull against the best hit.
+    const float x = (float)t;
+    return x + ::fabsf(x) * 4e-6f + 1e-30f;
+}
+
+// `stk` / `stkt`: this lane's columns of the LDS node / entry-distance stacks.
+template <class Real, bool COUNT>
+__device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
+                                                float* stkt, uint32_t* cnt) {
+    const FRay f = make_fray(r.o, r.d);
+    Real best_t = (Real)__builtin_inf();
+    int best = -1;
+    float thi = __builtin_inff();
+    float tn0;
+    if (COUNT) cnt[CT_NODE]++;
+    int node = 0;
+    if (!slab(S.fnodes[0], f, thi, tn0)) {
+        t_hit = best_t;
+        return -1;
+    }
+    int sp = 0;
+    while (true) {
+        const RtNode nd = S.fnodes[node];
+        bool next = false;
+        if (nd.b < 0) {
+            const int end = nd.a - nd.b;
+            for (int k = nd.a; k < end; ++k) {
+                Real t;
+                if (prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt) && (t < best_t || (t == best_t && k < best))) {
+                    best_t = t;
+                    best = k;
+                    thi = upper_f<Real>(t);
+                }
+            }
+        } else {
+            float ta, tb;
+            if (COUNT) cnt[CT_NODE] += 2;
+            const bool ha = slab(S.fnodes[nd.a], f, thi, ta);
+            const bool hb = slab(S.fnodes[nd.b], f, thi, tb);
+            if (ha && hb) {
+                const bool a_first = ta <= tb;
+                stk[sp * kBlock] = a_first ? nd.b : nd.a;
+                stkt[sp * kBlock] = a_first ? tb : ta;
+                ++sp;
+                node = a_first ? nd.a : nd.b;
+                next = true;
+            } else if (ha || hb) {
+                node = ha ? nd.a : nd.b;
+                next = true;
+            }
+        }
+        if (!next) {
+            while (sp > 0) {
+                --sp;
+                if (stkt[sp * kBlock] <= thi) {
+                    node = stk[sp * kBlock];
+                    next = true;
+                    break;
+                }
+            }
+            if (!next) break;
+        }
+    }
+    t_hit = best_t;
+    return best;
+}
+
 // ONBasis (src/geometry/onbasis.ts:18-51)
 struct Onb {
     V3 u, v, w;
@@ -457,13 +642,14 @@ __device__ __forceinline__ bool pixel_converged(const RtCamera& c, int n, double
     return ci <= c.a_tolerance * mean;
 }
 
-template <class Real, bool EMIT, bool COUNT>
+template <class Real, bool EMIT, bool COUNT, bool FAST>
 __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion reg, RenderOut out, int tiles_x,
                                                            int my_tiles) {
     extern __shared__ int lds_stack[];
     const RtCamera& C = S.cam;
     const int lane = threadIdx.x & (kWave - 1);
     int* stk = lds_stack + threadIdx.x;
+    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C.stack_depth * kBlock + threadIdx.x;
 
     const int endX = min(reg.x + reg.width, C.width);
     const int endY = min(reg.y + reg.height, C.height);
@@ -551,7 +737,8 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion 
                     const RayK<Real> ray = make_ray<Real>(o, d);
                     Real t;
                     if (COUNT) cnt[CT_RAYS]++;
-                    const int h = closest_hit<Real, COUNT>(S, ray, t, stk, cnt);
+                    const int h = FAST ? closest_hit_fast<Real, COUNT>(S, ray, t, stk, stkt, cnt)
+                                       : closest_hit<Real, COUNT>(S, ray, t, stk, cnt);
                     if (h < 0) {
                         term = true;
                         if (!C.has_background) st_err |= ERR_NO_BACKGROUND;

@@ -5,18 +5,22 @@
 
 namespace rt {
 
-template <bool EMIT, bool COUNT>
+template <bool EMIT, bool COUNT, bool FAST>
 static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                      hipStream_t stream) {
-    hipLaunchKernelGGL((pt_render_kernel<double, EMIT, COUNT>), dim3(g.grid), dim3(kBlock), g.lds_bytes, stream, S,
-                       reg, out, g.tiles_x, g.my_tiles);
+    hipLaunchKernelGGL((pt_render_kernel<double, EMIT, COUNT, FAST>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+                       stream, S, reg, out, g.tiles_x, g.my_tiles);
     return hipGetLastError();
 }
 
-hipError_t launch_render_ref(bool emit, bool count, const DevScene& S, const RtRegion& reg, const RenderOut& out,
+hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
                              const LaunchGeom& g, hipStream_t stream) {
-    if (emit) return count ? go<true, true>(S, reg, out, g, stream) : go<true, false>(S, reg, out, g, stream);
-    return count ? go<false, true>(S, reg, out, g, stream) : go<false, false>(S, reg, out, g, stream);
+    if (v.fast) {
+        if (v.emit) return v.count ? go<true, true, true>(S, reg, out, g, stream) : go<true, false, true>(S, reg, out, g, stream);
+        return v.count ? go<false, true, true>(S, reg, out, g, stream) : go<false, false, true>(S, reg, out, g, stream);
+    }
+    if (v.emit) return v.count ? go<true, true, false>(S, reg, out, g, stream) : go<true, false, false>(S, reg, out, g, stream);
+    return v.count ? go<false, true, false>(S, reg, out, g, stream) : go<false, false, false>(S, reg, out, g, stream);
 }
 
 __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long* counters,
@@ -34,8 +38,9 @@ hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* coun
 }
 
 // out per ray: {hit, t, p.xyz, n.xyz, front, prim}
+template <bool FAST>
 __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, const float* orig, const float* dir,
-                                                           double tmin_unused, double tmax_unused, double* out) {
+                                                           double* out) {
     extern __shared__ int lds_stack[];
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -43,7 +48,10 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
     const V3 d = v3(dir[3 * k], dir[3 * k + 1], dir[3 * k + 2]);
     const RayK<double> r = make_ray<double>(o, d);
     double t = 0;
-    const int h = closest_hit<double, false>(S, r, t, lds_stack + threadIdx.x, nullptr);
+    int* stk = lds_stack + threadIdx.x;
+    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)S.cam.stack_depth * kBlock + threadIdx.x;
+    const int h = FAST ? closest_hit_fast<double, false>(S, r, t, stk, stkt, nullptr)
+                       : closest_hit<double, false>(S, r, t, stk, nullptr);
     double* w = out + 10 * (size_t)k;
     w[0] = h >= 0;
     w[1] = h >= 0 ? t : 0.0;
@@ -69,11 +77,14 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
     }
 }
 
-hipError_t launch_world_hit_ref(const DevScene& S, int n, const float* orig, const float* dir, double tmin,
-                                double tmax, double* out, hipStream_t stream) {
+hipError_t launch_world_hit_ref(const DevScene& S, bool fast, int n, const float* orig, const float* dir,
+                                double* out, hipStream_t stream) {
     const int grid = (n + kBlock - 1) / kBlock;
-    const size_t lds = (size_t)S.cam.stack_depth * kBlock * sizeof(int);
-    hipLaunchKernelGGL(world_hit_kernel, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, tmin, tmax, out);
+    const size_t lds = stack_lds_bytes(S.cam.stack_depth, true);
+    if (fast)
+        hipLaunchKernelGGL(world_hit_kernel<true>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, out);
+    else
+        hipLaunchKernelGGL(world_hit_kernel<false>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, out);
     return hipGetLastError();
 }
 

@@ -50,11 +50,13 @@ int device_cus(int dev) {
 struct rt_camera {
     SceneBuild build;
     int32_t precision = PREC_REF;
+    int32_t traversal = TRAV_FAST;
     double mix_total = 0.5, light_w = 0.0;
     std::mutex mu;
 
     int device = -1;
     RtNode* d_nodes = nullptr;
+    RtNode* d_fnodes = nullptr;
     RtPrim* d_prims = nullptr;
     RtMat* d_mats = nullptr;
     RtLight* d_lights = nullptr;
@@ -72,7 +74,7 @@ struct rt_camera {
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
-        for (void* p : {(void*)d_nodes, (void*)d_prims, (void*)d_mats, (void*)d_lights, (void*)d_stats,
+        for (void* p : {(void*)d_nodes, (void*)d_fnodes, (void*)d_prims, (void*)d_mats, (void*)d_lights, (void*)d_stats,
                         (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad})
             if (p) (void)hipFree(p);
         (void)hipSetDevice(prev);
@@ -94,6 +96,7 @@ struct rt_camera {
         if (device == dev) return;
         if (device >= 0) release();
         d_nodes = upload(build.nodes);
+        d_fnodes = upload(build.fnodes);
         d_prims = upload(build.prims);
         d_mats = upload(build.mats);
         d_lights = upload(build.lights);
@@ -114,6 +117,7 @@ struct rt_camera {
     DevScene dev_scene() const {
         DevScene S;
         S.nodes = d_nodes;
+        S.fnodes = d_fnodes;
         S.prims = d_prims;
         S.mats = d_mats;
         S.lights = d_lights;
@@ -124,8 +128,8 @@ struct rt_camera {
     }
 
     // Launch one render; returns after queueing (and synchronising if asked).
-    void launch(const rt_region& region, int tile_group, int tile_groups, int prec, bool count, uint8_t* rgb,
-                float* rad, int32_t* pxs, int32_t* pxb, hipStream_t stream) {
+    void launch(const rt_region& region, int tile_group, int tile_groups, int prec, int trav, bool count,
+                uint8_t* rgb, float* rad, int32_t* pxs, int32_t* pxb, hipStream_t stream) {
         const RtCamera& C = build.cam;
         if (tile_groups < 1 || tile_group < 0 || tile_group >= tile_groups)
             throw std::invalid_argument("tile_group must satisfy 0 <= tile_group < tile_groups");
@@ -142,14 +146,14 @@ struct rt_camera {
         g.my_tiles = (int)mine;
         const long want = (mine + (kBlock / kWave) - 1) / (kBlock / kWave);
         g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus * 8));
-        g.lds_bytes = (size_t)std::max(C.stack_depth, 1) * kBlock * sizeof(int);
+        const KernelVariant v{C.emissive_scatter != 0, count, trav == TRAV_FAST && build.fast_ok};
+        g.lds_bytes = stack_lds_bytes(C.stack_depth, v.fast);
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
         if (mine == 0) return;
         const DevScene S = dev_scene();
-        const bool emit = C.emissive_scatter != 0;
-        hipError_t e = prec == PREC_FP32 ? launch_render_fp32(emit, count, S, reg, out, g, stream)
-                                         : launch_render_ref(emit, count, S, reg, out, g, stream);
+        hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, g, stream)
+                                         : launch_render_ref(v, S, reg, out, g, stream);
         hip_check(e, "pt_render_kernel launch");
     }
 
@@ -231,6 +235,17 @@ int rt_camera_create(const char* scene_json, const char* render_options_json, rt
             if (const rtj::Value* r = scene.get("render")) pick(r->get("precision"));
             if (rop) pick(rop->get("precision"));
             cam->precision = prec;
+            int32_t trav = TRAV_FAST;
+            auto pick_t = [&](const rtj::Value* v) {
+                if (v && v->is_string()) {
+                    if (v->str == "reference") trav = TRAV_REFERENCE;
+                    else if (v->str == "fast") trav = TRAV_FAST;
+                    else throw std::runtime_error("traversal must be 'fast' or 'reference'");
+                }
+            };
+            if (const rtj::Value* r = scene.get("render")) pick_t(r->get("traversal"));
+            if (rop) pick_t(rop->get("traversal"));
+            cam->traversal = trav;
             // MixturePDF([cosine, ...lights], [0.5, ...0.5/nL]).totalWeight (pdf.ts:48-52)
             const int nl = cam->build.cam.n_lights;
             cam->light_w = nl > 0 ? 0.5 / (double)nl : 0.0;
@@ -269,6 +284,8 @@ int rt_camera_get_info(const rt_camera* cam, rt_camera_info* info) {
     info->mode = C.mode;
     info->adaptive = C.adaptive;
     info->precision = cam->precision;
+    // effective traversal: the fast one only where it is provably exact (scene.cpp prims_inside_boxes)
+    info->traversal = (cam->traversal == TRAV_FAST && cam->build.fast_ok) ? TRAV_FAST : TRAV_REFERENCE;
     info->seed = C.seed;
     info->samples = C.samples;
     info->aperture = C.aperture;
@@ -293,7 +310,7 @@ int rt_camera_render_region(rt_camera* cam, const rt_region* region, uint8_t* rg
         cam->ensure_frame();
         const RtCamera& C = cam->build.cam;
         const hipStream_t stream = nullptr;
-        cam->launch(*region, 0, 1, cam->precision, false, rgb ? cam->d_rgb : nullptr,
+        cam->launch(*region, 0, 1, cam->precision, cam->traversal, false, rgb ? cam->d_rgb : nullptr,
                     radiance ? cam->d_rad : nullptr, nullptr, nullptr, stream);
         cam->read_stats(stats, nullptr, stream);
         // copy back only the region's rows/columns (the caller's buffer is the full frame)
@@ -335,7 +352,8 @@ int rt_camera_render_device(rt_camera* cam, const rt_launch* L, rt_render_stats*
         cam->ensure_device();
         const hipStream_t stream = (hipStream_t)L->stream;
         const int prec = L->precision < 0 ? cam->precision : L->precision;
-        cam->launch(L->region, L->tile_group, L->tile_groups, prec, L->count_work != 0, L->rgb, L->radiance,
+        const int trav = L->traversal < 0 ? cam->traversal : L->traversal;
+        cam->launch(L->region, L->tile_group, L->tile_groups, prec, trav, L->count_work != 0, L->rgb, L->radiance,
                     L->px_samples, L->px_bounces, stream);
         if (L->synchronize) cam->read_stats(stats, L->count_work ? work_counters : nullptr, stream);
         return RT_OK;
@@ -360,7 +378,8 @@ int rt_camera_export(const rt_camera* cam, void* nodes, void* prims, void* mater
     return RT_OK;
 }
 
-int rt_debug_world_hit(rt_camera* cam, int32_t n, const float* orig, const float* dir, double* out) {
+int rt_debug_world_hit(rt_camera* cam, int32_t traversal, int32_t n, const float* orig, const float* dir,
+                       double* out) {
     if (!cam || n < 0 || (n > 0 && (!orig || !dir || !out))) return set_error(RT_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lock(cam->mu);
     float* d_o = nullptr;
@@ -374,7 +393,8 @@ int rt_debug_world_hit(rt_camera* cam, int32_t n, const float* orig, const float
         hip_check(hipMalloc(&d_out, (size_t)n * 10 * sizeof(double)), "hipMalloc");
         hip_check(hipMemcpy(d_o, orig, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
         hip_check(hipMemcpy(d_d, dir, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
-        hip_check(launch_world_hit_ref(cam->dev_scene(), n, d_o, d_d, 0.001, INFINITY, d_out, nullptr),
+        const bool fast = (traversal < 0 ? cam->traversal : traversal) == TRAV_FAST && cam->build.fast_ok;
+        hip_check(launch_world_hit_ref(cam->dev_scene(), fast, n, d_o, d_d, d_out, nullptr),
                   "world_hit_kernel");
         hip_check(hipMemcpy(out, d_out, (size_t)n * 10 * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
         (void)hipFree(d_o);

@@ -834,6 +834,65 @@ int32_t loop_threshold(double x) {
 
 }  // namespace
 
+// Boxes for the fast traversal (pt_kernel.hpp closest_hit_fast). The
+// reference's AABB.hit never accepts a box that is inverted or flat on an
+// axis (its per-axis interval is empty), and always accepts one with a NaN
+// bound; a strict slab test would treat those differently, so they are
+// encoded as "always reject" (NaN in bmin[0]) and "always accept" (infinite
+// box). Every other box is padded outward by ~1e-6 relative, so the fp32
+// slab test can never cull a box the exact primitive tests would hit.
+std::vector<RtNode> make_fast_nodes(const std::vector<RtNode>& nodes) {
+    std::vector<RtNode> out(nodes);
+    for (RtNode& n : out) {
+        bool nan = false, empty = false;
+        for (int a = 0; a < 3; ++a) {
+            if (std::isnan(n.bmin[a]) || std::isnan(n.bmax[a])) nan = true;
+            else if (!(n.bmin[a] < n.bmax[a])) empty = true;
+        }
+        if (nan) {
+            for (int a = 0; a < 3; ++a) { n.bmin[a] = -INFINITY; n.bmax[a] = INFINITY; }
+        } else if (empty) {
+            n.bmin[0] = NAN;
+        } else {
+            for (int a = 0; a < 3; ++a) {
+                const double lo = n.bmin[a], hi = n.bmax[a];
+                if (std::isfinite(lo)) n.bmin[a] = std::nextafter((float)(lo - 1e-6 * (1.0 + std::fabs(lo))), -INFINITY);
+                if (std::isfinite(hi)) n.bmax[a] = std::nextafter((float)(hi + 1e-6 * (1.0 + std::fabs(hi))), INFINITY);
+            }
+        }
+    }
+    return out;
+}
+
+// The fast traversal is exact only if no primitive can be hit outside the box
+// the reference gives it: a negative-radius sphere (inverted box, e.g. the
+// default scene's hollow glass), a NaN bound, or a plane whose normal passes
+// the 0.9999 axis test without being exactly axis-aligned (thin slab box around
+// a tilted plane, src/entities/plane.ts:280-307). Such scenes use the
+// reference-order traversal.
+bool prims_inside_boxes(const std::vector<RtPrim>& prims) {
+    for (const RtPrim& p : prims) {
+        for (int k = 0; k < 4; ++k)
+            if (std::isnan(p.g0[k]) || std::isnan(p.g1[k]) || std::isnan(p.g2[k]) || std::isnan(p.g3[k]) ||
+                std::isnan(p.g4[k]))
+                return false;
+        if (std::isnan(p.s0)) return false;
+        if (p.type == PRIM_SPHERE) {
+            if (!(p.s0 > 0) || !std::isfinite(p.s0)) return false;
+        } else if (p.type == PRIM_PLANE) {
+            const double n[3] = {p.g3[0], p.g3[1], p.g3[2]};
+            for (int a = 0; a < 3; ++a) {
+                if (std::fabs(n[a]) > 0.9999) {
+                    const bool exact = std::fabs(n[a]) == 1.0 && n[(a + 1) % 3] == 0.0 && n[(a + 2) % 3] == 0.0;
+                    if (!exact) return false;
+                    break;
+                }
+            }
+        }
+    }
+    return true;
+}
+
 SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
     if (!scene_data.is_object()) fail("sceneData must be an object");
     Builder b(scene_data);
@@ -992,6 +1051,8 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
     cam.n_mats = (int32_t)b.out.mats.size();
     cam.seed = (uint32_t)(int64_t)seed;
     cam.stack_depth = b.out.bvh_depth + 1;
+    b.out.fnodes = make_fast_nodes(b.out.nodes);
+    b.out.fast_ok = prims_inside_boxes(b.out.prims);
     return std::move(b.out);
 }
 

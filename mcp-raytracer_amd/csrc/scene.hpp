@@ -119,11 +119,16 @@ struct RtRegion {
 // Host-side build product. Owned by rt_camera; uploaded to the device lazily.
 struct SceneBuild {
     std::vector<RtNode> nodes;
+    std::vector<RtNode> fnodes;  // same tree, boxes for the fast traversal (padded / reject-marked)
     std::vector<RtPrim> prims;
     std::vector<RtMat> mats;
     std::vector<RtLight> lights;
     RtCamera cam{};
     int bvh_depth = 0;
+    // Every primitive lies inside its own reference box (no negative / NaN
+    // sphere radius, no slightly tilted plane given a thin axis box), so a
+    // conservative culling test returns the reference's hit: fast traversal OK.
+    bool fast_ok = true;
     std::vector<int32_t> prim_object;  // prim slot -> index in SceneData.objects
 };
 

@@ -18,6 +18,7 @@ HEADER = Path(__file__).resolve().parents[2] / "include" / "rt_amd.h"
 
 RT_OK, RT_ERR_INVALID, RT_ERR_DEVICE, RT_ERR_RENDER = 0, 1, 2, 3
 PRECISION = {"ref": 0, "fp32": 1}
+TRAVERSAL = {"fast": 0, "reference": 1}
 
 CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_sphere",
             "bounces", "diffuse", "samples", "rays"]
@@ -41,14 +42,14 @@ class RtCameraInfo(C.Structure):
                 ("n_materials", C.c_int32), ("bvh_depth", C.c_int32),
                 ("samples_loop", C.c_int32), ("depth", C.c_int32), ("roulette", C.c_int32),
                 ("roulette_depth", C.c_int32), ("mode", C.c_int32), ("adaptive", C.c_int32),
-                ("precision", C.c_int32), ("seed", C.c_uint32),
+                ("precision", C.c_int32), ("traversal", C.c_int32), ("seed", C.c_uint32),
                 ("samples", C.c_double), ("aperture", C.c_double),
                 ("a_tolerance", C.c_double), ("a_batch", C.c_double)]
 
 
 class RtLaunch(C.Structure):
     _fields_ = [("region", RtRegion), ("tile_group", C.c_int32), ("tile_groups", C.c_int32),
-                ("precision", C.c_int32), ("count_work", C.c_int32),
+                ("precision", C.c_int32), ("traversal", C.c_int32), ("count_work", C.c_int32),
                 ("rgb", C.c_void_p), ("radiance", C.c_void_p),
                 ("px_samples", C.c_void_p), ("px_bounces", C.c_void_p),
                 ("stream", C.c_void_p), ("synchronize", C.c_int32)]
@@ -78,7 +79,7 @@ _SIGS = {
                                           C.POINTER(C.c_uint64)]),
     "rt_camera_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                    C.c_void_p]),
-    "rt_debug_world_hit": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_debug_world_hit": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_void_p]),
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
 }

@@ -147,7 +147,7 @@ class Camera:
 
     def render_device(self, *, rgb_ptr=None, radiance_ptr=None, region=None, tile_group=0, tile_groups=1,
                       precision: Optional[str] = None, stream=None, synchronize=False, count_work=False,
-                      px_samples_ptr=None, px_bounces_ptr=None):
+                      px_samples_ptr=None, px_bounces_ptr=None, traversal: Optional[str] = None):
         """Device-resident render into caller-owned device buffers (full-frame
         layout). Returns (RenderStats|None, work_counters|None)."""
         if region is None:
@@ -156,6 +156,7 @@ class Camera:
         L.region = _region(region)
         L.tile_group, L.tile_groups = int(tile_group), int(tile_groups)
         L.precision = -1 if precision is None else _lib.PRECISION[precision]
+        L.traversal = -1 if traversal is None else _lib.TRAVERSAL[traversal]
         L.count_work = 1 if count_work else 0
         L.rgb = rgb_ptr
         L.radiance = radiance_ptr
@@ -186,13 +187,14 @@ class Camera:
                                               prim_object.ctypes.data))
         return {"nodes": nodes, "prims": prims, "materials": mats, "lights": lights, "prim_object": prim_object}
 
-    def debug_world_hit(self, origins, directions):
+    def debug_world_hit(self, origins, directions, traversal: Optional[str] = None):
         """Closest hit of rays through the device BVH (ref precision)."""
         import numpy as np
         o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(directions, dtype=np.float32).reshape(-1, 3)
         out = np.zeros((o.shape[0], 10), dtype=np.float64)
-        _lib.check(self._lib.rt_debug_world_hit(self._h, o.shape[0], o.ctypes.data, d.ctypes.data,
+        tr = -1 if traversal is None else _lib.TRAVERSAL[traversal]
+        _lib.check(self._lib.rt_debug_world_hit(self._h, tr, o.shape[0], o.ctypes.data, d.ctypes.data,
                                                 out.ctypes.data))
         return out
 

@@ -108,3 +108,14 @@ def test_divide_into_regions_matches_reference(rt):
     regs = rt.divide_into_regions(10, 7, 3)
     assert [(r["y"], r["height"]) for r in regs] == [(0, 3), (3, 3), (6, 1)]
     assert len(rt.divide_into_regions(10, 2, 8)) == 2
+
+
+def test_fast_traversal_only_where_exact(rt):
+    """Scenes whose primitives can be hit outside their reference box (negative
+    radius sphere in the default scene) fall back to the reference traversal."""
+    assert rt.create_camera_from_scene_data(rt.generate_scene_data({"type": "cornell"})).info["traversal"] == 0
+    assert rt.create_camera_from_scene_data(rt.generate_scene_data({"type": "default"})).info["traversal"] == 1
+    sd = rt.generate_scene_data({"type": "rain", "options": {"seed": 1}})
+    assert rt.create_camera_from_scene_data(sd, {"traversal": "reference"}).info["traversal"] == 1
+    with pytest.raises(rt.RtError):
+        rt.create_camera_from_scene_data(sd, {"traversal": "sideways"})

@@ -186,7 +186,8 @@ def test_work_counters_match_oracle(rt, oracle, gpu):
     import torch
     sd = rt.generate_scene_data({"type": "cornell"})
     ro = {"width": 32, "samples": 8, "depth": 16, **NOADAPT}
-    cam = rt.create_camera_from_scene_data(sd, ro)
+    # reference-order traversal: the same node / primitive tests as the reference
+    cam = rt.create_camera_from_scene_data(sd, {**ro, "traversal": "reference"})
     buf = torch.zeros((32, 32, 3), dtype=torch.uint8, device="cuda")
     st, cnt = cam.render_device(rgb_ptr=buf.data_ptr(), synchronize=True, count_work=True)
     orc = oracle.render(sd, ro, counters=True)["counters"]
@@ -199,18 +200,36 @@ def test_world_hit_matches_oracle(rt, oracle, gpu):
     for cfg in [{"type": "spheres", "options": {"count": 200, "seed": 3}}, {"type": "cornell"}, {"type": "default"}]:
         sd = rt.generate_scene_data(cfg)
         cam = rt.create_camera_from_scene_data(sd, {"width": 8})
-        n = 2000
+        n = 4000
         o = rng.uniform(-1.5, 1.5, (n, 3)).astype(np.float32) + np.float32([0, 0.5, 0])
         d = rng.normal(size=(n, 3)).astype(np.float32)
-        g = cam.debug_world_hit(o, d)
+        d[: n // 8, rng.integers(0, 3)] = 0  # axis-parallel rays: 1/0 in the slab tests
         c = oracle.world_hit(sd, o, d)
-        assert np.array_equal(g[:, 0], c[:, 0])
-        h = g[:, 0] > 0
-        assert np.array_equal(g[h, 1], c[h, 1])
-        assert np.array_equal(g[h, 2:9], c[h, 2:9])
-        # prim slot -> SceneData object index
         po = cam.export()["prim_object"]
-        assert np.array_equal(po[g[h, 9].astype(int)], c[h, 9].astype(int))
+        for trav in ["reference", "fast"]:
+            g = cam.debug_world_hit(o, d, traversal=trav)
+            assert np.array_equal(g[:, 0], c[:, 0]), trav
+            h = g[:, 0] > 0
+            assert np.array_equal(g[h, 1], c[h, 1]), trav
+            assert np.array_equal(g[h, 2:9], c[h, 2:9]), trav
+            # prim slot -> SceneData object index
+            assert np.array_equal(po[g[h, 9].astype(int)], c[h, 9].astype(int)), trav
+
+
+@pytest.mark.parametrize("name", ["cornell", "spheres", "rain", "default"])
+def test_fast_traversal_equals_reference_traversal(rt, gpu, name):
+    """Larger images than the oracle can render quickly: the fast traversal
+    must reproduce the reference-order traversal bit-for-bit."""
+    cfg, ro = _cfgs()[name]
+    sd = rt.generate_scene_data(cfg)
+    ro = {**ro, "width": 192, "samples": 16}
+    outs = []
+    for trav in ["reference", "fast"]:
+        cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
+        outs.append((rgb, rad, st))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1], equal_nan=True)
+    assert outs[0][2].bounces == outs[1][2].bounces
 
 
 def test_missing_background_raises_like_reference(rt, gpu):
