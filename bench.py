@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--depth", type=int, default=16)
     ap.add_argument("--precision", default="ref", choices=["ref", "fp32"])
     ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "fast", "reference"],
+                    help="closest-hit strategy (all bit-identical; auto = brute force up to 16 primitives)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="JSON with measured HBM bytes per launch (from rocprofv3 --pmc)")
@@ -97,7 +99,7 @@ def main():
     cfg, extra = SCENES[args.scene]
     scene_data = rt.generate_scene_data(cfg)
     ropts = {"width": args.width, "samples": args.spp, "depth": args.depth, "aTolerance": 0,
-             "seed": args.seed, "precision": args.precision, **extra}
+             "seed": args.seed, "precision": args.precision, "traversal": args.traversal, **extra}
     cam = rt.create_camera_from_scene_data(scene_data, ropts)
     W, H = cam.image_width, cam.image_height
     dev = torch.device("cuda", local_rank)
@@ -105,10 +107,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
-    # Algorithmic work of this rank's launch: one instrumented (untimed) launch;
-    # identical seeds => identical paths to every timed launch.
+    # Algorithmic work of this rank's launch: the node / primitive
+    # / material / light-PDF work the REFERENCE algorithm does on this workload,
+    # counted by one instrumented, untimed launch with the reference-order
+    # traversal (its counts equal the oracle's: test_work_counters_match_oracle).
+    # Identical seeds => identical paths to every timed launch, whatever the
+    # closest-hit strategy, so this is a fixed per-workload figure.
     _, counters = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world,
-                                    stream=sptr, synchronize=True, count_work=True)
+                                    stream=sptr, synchronize=True, count_work=True, traversal="reference")
     st, _ = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr,
                               synchronize=True)
     my_pixels = int(st.pixels)
@@ -161,7 +167,8 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(scene_data, {k: v for k, v in ropts.items() if k != "precision"}, W, H, args.spp)
+            cpu = cpu_baseline(scene_data, {k: v for k, v in ropts.items() if k not in ("precision", "traversal")},
+                               W, H, args.spp)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -172,6 +179,7 @@ def main():
             "config": {"workload": f"{args.scene} {W}x{H} spp={args.spp} depth={args.depth}",
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "depth": args.depth,
                        "precision": args.precision, "adaptive": False,
+                       "traversal": ["fast", "reference", "brute"][cam.info["traversal"]],
                        "parallelism": f"8x8-tile interleave x{world} + RCCL reduce to rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

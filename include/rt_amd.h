@@ -42,11 +42,15 @@ enum {
 };
 
 enum { RT_PRECISION_REF = 0, RT_PRECISION_FP32 = 1 };
-/* BVH traversal. Both return the reference's closest hit bit-for-bit:
+/* Closest-hit strategy. All return the reference's closest hit bit-for-bit:
  * REFERENCE visits nodes in BVHNode.hit's order with AABB.hit's per-axis test
  * (src/geometry/bvh.ts:128-146); FAST culls with a strict slab test on padded
- * boxes, near child first, and breaks t ties by leaf order. */
-enum { RT_TRAVERSAL_FAST = 0, RT_TRAVERSAL_REFERENCE = 1 };
+ * boxes, near child first, and breaks t ties by leaf order; BRUTE tests every
+ * primitive in leaf order (small scenes). AUTO (default) = BRUTE up to 16
+ * primitives, else FAST. FAST/BRUTE fall back to REFERENCE for scenes where a
+ * primitive can be hit outside its reference box (rt_camera_info.traversal
+ * reports the strategy in effect). */
+enum { RT_TRAVERSAL_FAST = 0, RT_TRAVERSAL_REFERENCE = 1, RT_TRAVERSAL_BRUTE = 2, RT_TRAVERSAL_AUTO = 3 };
 
 typedef struct rt_camera rt_camera;
 
@@ -81,7 +85,7 @@ typedef struct {
     rt_region region;
     int32_t tile_group, tile_groups;
     int32_t precision;       /* -1: the camera's precision */
-    int32_t traversal;       /* -1: the camera's; RT_TRAVERSAL_FAST / RT_TRAVERSAL_REFERENCE */
+    int32_t traversal;       /* -1: the camera's; else an RT_TRAVERSAL_* value */
     int32_t count_work;      /* 1: instrumented build, fills work_counters */
     uint8_t* rgb;            /* device, may be NULL */
     float* radiance;         /* device, may be NULL */

@@ -10,7 +10,6 @@
 namespace rt {
 
 enum Precision : int32_t { PREC_REF = 0, PREC_FP32 = 1 };
-enum Traversal : int32_t { TRAV_FAST = 0, TRAV_REFERENCE = 1 };
 
 struct LaunchGeom {
     int tiles_x;
@@ -22,7 +21,7 @@ struct LaunchGeom {
 struct KernelVariant {
     bool emit;   // emission stack (a scattering material emits)
     bool count;  // work counters
-    bool fast;   // fast traversal (same result) vs reference-order traversal
+    int trav;    // TRAV_FAST / TRAV_REFERENCE / TRAV_BRUTE (resolved, never AUTO)
 };
 
 hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
@@ -33,13 +32,14 @@ hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const R
 hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* counters, unsigned int* tile_counter,
                              hipStream_t stream);
 // Closest hit through the device traversal for a batch of rays (parity tests).
-hipError_t launch_world_hit_ref(const DevScene& S, bool fast, int n, const float* orig, const float* dir,
+hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float* orig, const float* dir,
                                 double* out, hipStream_t stream);
 
 // LDS bytes per 256-thread block for the traversal stack.
-inline size_t stack_lds_bytes(int stack_depth, bool fast) {
+inline size_t stack_lds_bytes(int stack_depth, int trav) {
+    if (trav == TRAV_BRUTE) return 0;
     const size_t d = (size_t)(stack_depth > 0 ? stack_depth : 1);
-    return d * kBlock * (fast ? 2 * sizeof(int) : sizeof(int));
+    return d * kBlock * (trav == TRAV_FAST ? 2 * sizeof(int) : sizeof(int));
 }
 
 }  // namespace rt

@@ -4,22 +4,26 @@
 
 namespace rt {
 
-template <bool EMIT, bool COUNT, bool FAST>
+template <bool EMIT, bool COUNT, int TRAV>
 static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                      hipStream_t stream) {
-    hipLaunchKernelGGL((pt_render_kernel<float, EMIT, COUNT, FAST>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+    hipLaunchKernelGGL((pt_render_kernel<float, EMIT, COUNT, TRAV>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
                        stream, S, reg, out, g.tiles_x, g.my_tiles);
     return hipGetLastError();
 }
 
+template <int TRAV>
+static hipError_t go_t(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
+                       const LaunchGeom& g, hipStream_t stream) {
+    if (v.emit) return v.count ? go<true, true, TRAV>(S, reg, out, g, stream) : go<true, false, TRAV>(S, reg, out, g, stream);
+    return v.count ? go<false, true, TRAV>(S, reg, out, g, stream) : go<false, false, TRAV>(S, reg, out, g, stream);
+}
+
 hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                              const LaunchGeom& g, hipStream_t stream) {
-    if (v.fast) {
-        if (v.emit) return v.count ? go<true, true, true>(S, reg, out, g, stream) : go<true, false, true>(S, reg, out, g, stream);
-        return v.count ? go<false, true, true>(S, reg, out, g, stream) : go<false, false, true>(S, reg, out, g, stream);
-    }
-    if (v.emit) return v.count ? go<true, true, false>(S, reg, out, g, stream) : go<true, false, false>(S, reg, out, g, stream);
-    return v.count ? go<false, true, false>(S, reg, out, g, stream) : go<false, false, false>(S, reg, out, g, stream);
+                             const LaunchGeom& g, hipStream_t stream) {
+    if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, stream);
+    if (v.trav == TRAV_FAST) return go_t<TRAV_FAST>(v, S, reg, out, g, stream);
+    return go_t<TRAV_REFERENCE>(v, S, reg, out, g, stream);
 }
 
 }  // namespace rt

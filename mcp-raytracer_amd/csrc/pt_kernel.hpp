@@ -63,6 +63,11 @@ struct RenderOut {
     unsigned int* tile_counter;
 };
 
+// Closest-hit strategies; all return the reference's hit bit-for-bit (see the
+// functions below). AUTO is resolved on the host.
+enum Traversal : int32_t { TRAV_FAST = 0, TRAV_REFERENCE = 1, TRAV_BRUTE = 2, TRAV_AUTO = 3 };
+constexpr int kBruteMaxPrims = 16;  // AUTO picks BRUTE up to this many primitives
+
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kTile = 8;          // 8x8 pixels per wave-tile
@@ -101,8 +106,21 @@ __device__ __forceinline__ double m_cos(double x) { return ::cos(x); }
 __device__ __forceinline__ float m_cos(float x) { return ::cosf(x); }
 __device__ __forceinline__ double m_sin(double x) { return ::sin(x); }
 __device__ __forceinline__ float m_sin(float x) { return ::sinf(x); }
-__device__ __forceinline__ double m_pow(double x, double y) { return ::pow(x, y); }
-__device__ __forceinline__ float m_pow(float x, float y) { return ::powf(x, y); }
+// Math.pow(x, 5) of Schlick's approximation (src/materials/dielectric.ts:98),
+// correctly rounded: x^5 in double-double (exact x^2 and x^4 products via FMA),
+// then one rounding. V8's and glibc's pow are within 1 ulp of this value (and
+// differ from it for ~0.1 % of arguments); it only feeds `reflectance > xi`.
+// The oracle computes the same correctly rounded value independently (binary128).
+__device__ __forceinline__ double pow5(double x) {
+    const double h2 = x * x, l2 = ::fma(x, x, -h2);
+    const double h4 = h2 * h2, l4 = ::fma(h2, h2, -h4) + 2.0 * h2 * l2;
+    const double h5 = h4 * x, l5 = ::fma(h4, x, -h5) + l4 * x;
+    return h5 + l5;
+}
+__device__ __forceinline__ float pow5(float x) {
+    const float x2 = x * x;
+    return x2 * x2 * x;
+}
 __device__ __forceinline__ double m_abs(double x) { return ::fabs(x); }
 __device__ __forceinline__ float m_abs(float x) { return ::fabsf(x); }
 __device__ __forceinline__ double m_sqrt(double x) { return ::sqrt(x); }
@@ -442,6 +460,30 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     return best;
 }
 
+// Small scenes: test every primitive in leaf order. The answer is the same
+// lexicographic minimum of (t, leaf slot) the fast traversal returns (valid
+// under the same condition, SceneBuild::fast_ok). The loop bound and the
+// primitive index are wave-uniform, so primitive records come through scalar
+// loads and no lane waits on a BVH stack.
+template <class Real, bool COUNT>
+__device__ __forceinline__ int closest_hit_brute(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
+                                                 uint32_t* cnt) {
+    const FRay f = make_fray(r.o, r.d);
+    Real best_t = (Real)__builtin_inf();
+    int best = -1;
+    float thi = __builtin_inff();
+    for (int k = 0; k < n_prims; ++k) {
+        Real t;
+        if (prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt) && t < best_t) {
+            best_t = t;
+            best = k;
+            thi = upper_f<Real>(t);
+        }
+    }
+    t_hit = best_t;
+    return best;
+}
+
 // ONBasis (src/geometry/onbasis.ts:18-51)
 struct Onb {
     V3 u, v, w;
@@ -485,7 +527,7 @@ __device__ __forceinline__ V3 dielectric_dir(Real ior, bool front, V3 din, V3 n,
     if (!refl) {
         Real r0 = ((Real)1 - ratio) / ((Real)1 + ratio);
         r0 = r0 * r0;
-        const Real reflectance = r0 + ((Real)1 - r0) * m_pow((Real)1 - cosT, (Real)5);
+        const Real reflectance = r0 + ((Real)1 - r0) * pow5((Real)1 - cosT);
         refl = reflectance > uniform<Real>(rng);
     }
     reflected = refl;
@@ -642,7 +684,27 @@ __device__ __forceinline__ bool pixel_converged(const RtCamera& c, int n, double
     return ci <= c.a_tolerance * mean;
 }
 
-template <class Real, bool EMIT, bool COUNT, bool FAST>
+// The camera/options block as seen through an opaque kernarg pointer. Reading
+// it this way inside the path loop stops the compiler from hoisting ~30 fp64
+// conversions of loop-invariant camera fields into VGPRs for the whole kernel
+// (the kernarg segment is constant memory: these are cheap scalar loads).
+typedef const __attribute__((address_space(4))) char* KArgPtr;
+__device__ __forceinline__ const RtCamera& cam_opaque() {
+    KArgPtr p = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const RtCamera*)(p + offsetof(DevScene, cam));  // addrspacecast; inferred back to constant
+}
+
+template <class Real, bool COUNT, int TRAV>
+__device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t, int* stk,
+                                               float* stkt, uint32_t* cnt) {
+    if (TRAV == TRAV_BRUTE) return closest_hit_brute<Real, COUNT>(S, n_prims, r, t, cnt);
+    if (TRAV == TRAV_FAST) return closest_hit_fast<Real, COUNT>(S, r, t, stk, stkt, cnt);
+    return closest_hit<Real, COUNT>(S, r, t, stk, cnt);
+}
+
+// Kernel arguments: S must stay the first parameter (cam_opaque reads it at kernarg offset 0).
+template <class Real, bool EMIT, bool COUNT, int TRAV>
 __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion reg, RenderOut out, int tiles_x,
                                                            int my_tiles) {
     extern __shared__ int lds_stack[];
@@ -690,6 +752,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion 
         int em_n = 0;
 
         while (active) {
+            const RtCamera& C = cam_opaque();
             if (new_path) {
                 rng = rng_init(C.seed, pix, (uint32_t)n);
                 // getRay (src/camera.ts:176-210)
@@ -737,8 +800,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion 
                     const RayK<Real> ray = make_ray<Real>(o, d);
                     Real t;
                     if (COUNT) cnt[CT_RAYS]++;
-                    const int h = FAST ? closest_hit_fast<Real, COUNT>(S, ray, t, stk, stkt, cnt)
-                                       : closest_hit<Real, COUNT>(S, ray, t, stk, cnt);
+                    const int h = closest_hit_any<Real, COUNT, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
                     if (h < 0) {
                         term = true;
                         if (!C.has_background) st_err |= ERR_NO_BACKGROUND;

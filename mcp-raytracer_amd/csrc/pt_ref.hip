@@ -5,22 +5,26 @@
 
 namespace rt {
 
-template <bool EMIT, bool COUNT, bool FAST>
+template <bool EMIT, bool COUNT, int TRAV>
 static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                      hipStream_t stream) {
-    hipLaunchKernelGGL((pt_render_kernel<double, EMIT, COUNT, FAST>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+    hipLaunchKernelGGL((pt_render_kernel<double, EMIT, COUNT, TRAV>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
                        stream, S, reg, out, g.tiles_x, g.my_tiles);
     return hipGetLastError();
 }
 
+template <int TRAV>
+static hipError_t go_t(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
+                       const LaunchGeom& g, hipStream_t stream) {
+    if (v.emit) return v.count ? go<true, true, TRAV>(S, reg, out, g, stream) : go<true, false, TRAV>(S, reg, out, g, stream);
+    return v.count ? go<false, true, TRAV>(S, reg, out, g, stream) : go<false, false, TRAV>(S, reg, out, g, stream);
+}
+
 hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
                              const LaunchGeom& g, hipStream_t stream) {
-    if (v.fast) {
-        if (v.emit) return v.count ? go<true, true, true>(S, reg, out, g, stream) : go<true, false, true>(S, reg, out, g, stream);
-        return v.count ? go<false, true, true>(S, reg, out, g, stream) : go<false, false, true>(S, reg, out, g, stream);
-    }
-    if (v.emit) return v.count ? go<true, true, false>(S, reg, out, g, stream) : go<true, false, false>(S, reg, out, g, stream);
-    return v.count ? go<false, true, false>(S, reg, out, g, stream) : go<false, false, false>(S, reg, out, g, stream);
+    if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, stream);
+    if (v.trav == TRAV_FAST) return go_t<TRAV_FAST>(v, S, reg, out, g, stream);
+    return go_t<TRAV_REFERENCE>(v, S, reg, out, g, stream);
 }
 
 __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long* counters,
@@ -38,7 +42,7 @@ hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* coun
 }
 
 // out per ray: {hit, t, p.xyz, n.xyz, front, prim}
-template <bool FAST>
+template <int TRAV>
 __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, const float* orig, const float* dir,
                                                            double* out) {
     extern __shared__ int lds_stack[];
@@ -50,8 +54,7 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
     double t = 0;
     int* stk = lds_stack + threadIdx.x;
     float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)S.cam.stack_depth * kBlock + threadIdx.x;
-    const int h = FAST ? closest_hit_fast<double, false>(S, r, t, stk, stkt, nullptr)
-                       : closest_hit<double, false>(S, r, t, stk, nullptr);
+    const int h = closest_hit_any<double, false, TRAV>(S, S.cam.n_prims, r, t, stk, stkt, nullptr);
     double* w = out + 10 * (size_t)k;
     w[0] = h >= 0;
     w[1] = h >= 0 ? t : 0.0;
@@ -77,14 +80,17 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
     }
 }
 
-hipError_t launch_world_hit_ref(const DevScene& S, bool fast, int n, const float* orig, const float* dir,
+hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float* orig, const float* dir,
                                 double* out, hipStream_t stream) {
     const int grid = (n + kBlock - 1) / kBlock;
-    const size_t lds = stack_lds_bytes(S.cam.stack_depth, true);
-    if (fast)
-        hipLaunchKernelGGL(world_hit_kernel<true>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, out);
+    const size_t lds = stack_lds_bytes(S.cam.stack_depth, TRAV_FAST);  // largest footprint
+    if (trav == TRAV_BRUTE)
+        hipLaunchKernelGGL(world_hit_kernel<TRAV_BRUTE>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, out);
+    else if (trav == TRAV_FAST)
+        hipLaunchKernelGGL(world_hit_kernel<TRAV_FAST>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, out);
     else
-        hipLaunchKernelGGL(world_hit_kernel<false>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, out);
+        hipLaunchKernelGGL(world_hit_kernel<TRAV_REFERENCE>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir,
+                           out);
     return hipGetLastError();
 }
 

@@ -50,7 +50,7 @@ int device_cus(int dev) {
 struct rt_camera {
     SceneBuild build;
     int32_t precision = PREC_REF;
-    int32_t traversal = TRAV_FAST;
+    int32_t traversal = TRAV_AUTO;
     double mix_total = 0.5, light_w = 0.0;
     std::mutex mu;
 
@@ -114,6 +114,14 @@ struct rt_camera {
         hip_check(hipMalloc(&d_rad, std::max<size_t>(px * 3, 1) * sizeof(float)), "hipMalloc");
     }
 
+    // The strategy a launch actually uses: BRUTE/FAST are exact only where every
+    // primitive lies inside its reference box (scene.cpp prims_inside_boxes).
+    int effective_traversal(int trav) const {
+        if (!build.fast_ok) return TRAV_REFERENCE;
+        if (trav == TRAV_AUTO) return build.cam.n_prims <= kBruteMaxPrims ? TRAV_BRUTE : TRAV_FAST;
+        return trav;
+    }
+
     DevScene dev_scene() const {
         DevScene S;
         S.nodes = d_nodes;
@@ -146,8 +154,8 @@ struct rt_camera {
         g.my_tiles = (int)mine;
         const long want = (mine + (kBlock / kWave) - 1) / (kBlock / kWave);
         g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus * 8));
-        const KernelVariant v{C.emissive_scatter != 0, count, trav == TRAV_FAST && build.fast_ok};
-        g.lds_bytes = stack_lds_bytes(C.stack_depth, v.fast);
+        const KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
+        g.lds_bytes = stack_lds_bytes(C.stack_depth, v.trav);
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
         if (mine == 0) return;
@@ -235,12 +243,14 @@ int rt_camera_create(const char* scene_json, const char* render_options_json, rt
             if (const rtj::Value* r = scene.get("render")) pick(r->get("precision"));
             if (rop) pick(rop->get("precision"));
             cam->precision = prec;
-            int32_t trav = TRAV_FAST;
+            int32_t trav = TRAV_AUTO;
             auto pick_t = [&](const rtj::Value* v) {
                 if (v && v->is_string()) {
                     if (v->str == "reference") trav = TRAV_REFERENCE;
                     else if (v->str == "fast") trav = TRAV_FAST;
-                    else throw std::runtime_error("traversal must be 'fast' or 'reference'");
+                    else if (v->str == "brute") trav = TRAV_BRUTE;
+                    else if (v->str == "auto") trav = TRAV_AUTO;
+                    else throw std::runtime_error("traversal must be 'auto', 'fast', 'brute' or 'reference'");
                 }
             };
             if (const rtj::Value* r = scene.get("render")) pick_t(r->get("traversal"));
@@ -284,8 +294,8 @@ int rt_camera_get_info(const rt_camera* cam, rt_camera_info* info) {
     info->mode = C.mode;
     info->adaptive = C.adaptive;
     info->precision = cam->precision;
-    // effective traversal: the fast one only where it is provably exact (scene.cpp prims_inside_boxes)
-    info->traversal = (cam->traversal == TRAV_FAST && cam->build.fast_ok) ? TRAV_FAST : TRAV_REFERENCE;
+    // effective traversal: fast/brute only where provably exact (scene.cpp prims_inside_boxes)
+    info->traversal = cam->effective_traversal(cam->traversal);
     info->seed = C.seed;
     info->samples = C.samples;
     info->aperture = C.aperture;
@@ -393,8 +403,8 @@ int rt_debug_world_hit(rt_camera* cam, int32_t traversal, int32_t n, const float
         hip_check(hipMalloc(&d_out, (size_t)n * 10 * sizeof(double)), "hipMalloc");
         hip_check(hipMemcpy(d_o, orig, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
         hip_check(hipMemcpy(d_d, dir, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
-        const bool fast = (traversal < 0 ? cam->traversal : traversal) == TRAV_FAST && cam->build.fast_ok;
-        hip_check(launch_world_hit_ref(cam->dev_scene(), fast, n, d_o, d_d, d_out, nullptr),
+        const int trav = cam->effective_traversal(traversal < 0 ? cam->traversal : traversal);
+        hip_check(launch_world_hit_ref(cam->dev_scene(), trav, n, d_o, d_d, d_out, nullptr),
                   "world_hit_kernel");
         hip_check(hipMemcpy(out, d_out, (size_t)n * 10 * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
         (void)hipFree(d_o);

@@ -18,7 +18,7 @@ HEADER = Path(__file__).resolve().parents[2] / "include" / "rt_amd.h"
 
 RT_OK, RT_ERR_INVALID, RT_ERR_DEVICE, RT_ERR_RENDER = 0, 1, 2, 3
 PRECISION = {"ref": 0, "fp32": 1}
-TRAVERSAL = {"fast": 0, "reference": 1}
+TRAVERSAL = {"fast": 0, "reference": 1, "brute": 2, "auto": 3}
 
 CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_sphere",
             "bounces", "diffuse", "samples", "rays"]

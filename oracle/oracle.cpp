@@ -28,9 +28,9 @@
 // the reference itself is statistical only. Third-party gl-matrix 3.4.3
 // (package-lock.json:3694) is restated from its published source: normalize =
 // a * (1/sqrt(|a|²)) when |a|² > 0, length = Math.hypot (V8 algorithm).
-// Transcendentals (Math.cos/sin/tan/pow/log10) use the C library here, which
+// Transcendentals (Math.cos/sin/tan/log10) use the C library here, which
 // may differ from V8's fdlibm ports in the last ulp: parity unpinned at that
-// level.
+// level. Schlick's Math.pow(x, 5) is evaluated correctly rounded (R_pow5).
 // ============================================================================
 #include <algorithm>
 #include <atomic>
@@ -208,6 +208,17 @@ template <class R> static inline R R_sqrt(R x) { return std::sqrt(x); }
 template <class R> static inline R R_cos(R x) { return std::cos(x); }
 template <class R> static inline R R_sin(R x) { return std::sin(x); }
 template <class R> static inline R R_pow(R x, R y) { return std::pow(x, y); }
+// Schlick's Math.pow(x, 5) (src/materials/dielectric.ts:98) in ref mode:
+// the correctly rounded x^5, formed in binary128 and rounded once. V8's fdlibm
+// pow and glibc's pow are each within 1 ulp of it (neither is correctly
+// rounded: glibc differs for ~0.1 % of arguments in [0, 1]); the product
+// computes the same value by a different route (double-double).
+static inline double R_pow5(double x) {
+    __float128 q = (__float128)x;
+    q = q * q * q * q * q;
+    return (double)q;
+}
+static inline float R_pow5(float x) { return std::pow(x, 5.0f); }
 
 static double hypot3_v8(double x, double y, double z) {
     double in[3] = {x, y, z}, ab[3] = {0, 0, 0};
@@ -448,7 +459,7 @@ template <class R> struct Dielectric : Material<R> {
     static R reflectance(R cosine, R ratio) {
         R r0 = (1 - ratio) / (1 + ratio);
         r0 = r0 * r0;
-        return r0 + (1 - r0) * R_pow<R>((1 - cosine), (R)5);
+        return r0 + (1 - r0) * R_pow5((R)(1 - cosine));
     }
     ScatterResult<R> scatter(const Ray<R>& rIn, const HitRecord<R>& rec) const override {
         Vec3<R> att = Vec3<R>::create(1.0, 1.0, 1.0);

@@ -113,9 +113,14 @@ def test_divide_into_regions_matches_reference(rt):
 def test_fast_traversal_only_where_exact(rt):
     """Scenes whose primitives can be hit outside their reference box (negative
     radius sphere in the default scene) fall back to the reference traversal."""
-    assert rt.create_camera_from_scene_data(rt.generate_scene_data({"type": "cornell"})).info["traversal"] == 0
+    cornell = rt.generate_scene_data({"type": "cornell"})  # 8 primitives: AUTO -> brute force
+    assert rt.create_camera_from_scene_data(cornell).info["traversal"] == 2
+    assert rt.create_camera_from_scene_data(cornell, {"traversal": "fast"}).info["traversal"] == 0
     assert rt.create_camera_from_scene_data(rt.generate_scene_data({"type": "default"})).info["traversal"] == 1
-    sd = rt.generate_scene_data({"type": "rain", "options": {"seed": 1}})
+    assert rt.create_camera_from_scene_data(rt.generate_scene_data({"type": "default"}),
+                                            {"traversal": "brute"}).info["traversal"] == 1
+    sd = rt.generate_scene_data({"type": "rain", "options": {"seed": 1}})  # 21 primitives: AUTO -> fast
+    assert rt.create_camera_from_scene_data(sd).info["traversal"] == 0
     assert rt.create_camera_from_scene_data(sd, {"traversal": "reference"}).info["traversal"] == 1
     with pytest.raises(rt.RtError):
         rt.create_camera_from_scene_data(sd, {"traversal": "sideways"})

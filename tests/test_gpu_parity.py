@@ -206,7 +206,7 @@ def test_world_hit_matches_oracle(rt, oracle, gpu):
         d[: n // 8, rng.integers(0, 3)] = 0  # axis-parallel rays: 1/0 in the slab tests
         c = oracle.world_hit(sd, o, d)
         po = cam.export()["prim_object"]
-        for trav in ["reference", "fast"]:
+        for trav in ["reference", "fast", "brute"]:
             g = cam.debug_world_hit(o, d, traversal=trav)
             assert np.array_equal(g[:, 0], c[:, 0]), trav
             h = g[:, 0] > 0
@@ -218,18 +218,20 @@ def test_world_hit_matches_oracle(rt, oracle, gpu):
 
 @pytest.mark.parametrize("name", ["cornell", "spheres", "rain", "default"])
 def test_fast_traversal_equals_reference_traversal(rt, gpu, name):
-    """Larger images than the oracle can render quickly: the fast traversal
-    must reproduce the reference-order traversal bit-for-bit."""
+    """Larger images than the oracle can render quickly: the fast and the
+    brute-force closest hit must reproduce the reference-order traversal
+    bit-for-bit."""
     cfg, ro = _cfgs()[name]
     sd = rt.generate_scene_data(cfg)
     ro = {**ro, "width": 192, "samples": 16}
     outs = []
-    for trav in ["reference", "fast"]:
+    for trav in ["reference", "fast", "brute"]:
         cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
         outs.append((rgb, rad, st))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1], equal_nan=True)
-    assert outs[0][2].bounces == outs[1][2].bounces
+    for k in (1, 2):
+        assert np.array_equal(outs[0][0], outs[k][0])
+        assert np.array_equal(outs[0][1], outs[k][1], equal_nan=True)
+        assert outs[0][2].bounces == outs[k][2].bounces
 
 
 def test_missing_background_raises_like_reference(rt, gpu):
