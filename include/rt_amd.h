@@ -86,7 +86,7 @@ typedef struct {
     int32_t tile_group, tile_groups;
     int32_t precision;       /* -1: the camera's precision */
     int32_t traversal;       /* -1: the camera's; else an RT_TRAVERSAL_* value */
-    int32_t count_work;      /* 1: instrumented build, fills work_counters */
+    int32_t count_work;      /* 1: instrumented build, fills work_counters; 2: section-timing diagnostic */
     uint8_t* rgb;            /* device, may be NULL */
     float* radiance;         /* device, may be NULL */
     int32_t* px_samples;     /* device W*H, may be NULL */
@@ -100,6 +100,14 @@ enum {
     RT_CT_NODE = 0, RT_CT_SPHERE, RT_CT_QUAD, RT_CT_PLANE, RT_CT_MATERIAL, RT_CT_LIGHT_QUAD,
     RT_CT_LIGHT_SPHERE, RT_CT_BOUNCES, RT_CT_DIFFUSE, RT_CT_SAMPLES, RT_CT_RAYS, RT_CT_WORDS
 };
+/* count_work == 2 (diagnostic): wave-cycles (s_memtime) per path-loop section,
+ * summed over waves, at work_counters[RT_CT_WORDS + RT_PR_*]. */
+enum {
+    RT_PR_NEWPATH = 0, RT_PR_RR, RT_PR_HIT, RT_PR_MISS, RT_PR_HITREC, RT_PR_SCATTER, RT_PR_SAMPLE, RT_PR_PDF,
+    RT_PR_ACC, RT_PR_TILE, RT_PR_LOOP, RT_PR_TRIPS, RT_PR_WORDS
+};
+/* work_counters arrays passed to rt_camera_render_device hold this many entries. */
+#define RT_COUNTER_WORDS 32
 
 int rt_version(void);
 const char* rt_last_error(void);
@@ -125,7 +133,7 @@ int rt_camera_render_region(rt_camera* cam, const rt_region* region, uint8_t* rg
 /* Camera.render (src/camera.ts:439-446): the whole image. */
 int rt_camera_render(rt_camera* cam, uint8_t* rgb, float* radiance, rt_render_stats* stats);
 
-/* Device-resident render (see rt_launch). stats / work_counters (RT_CT_WORDS
+/* Device-resident render (see rt_launch). stats / work_counters (RT_COUNTER_WORDS
  * u64) are filled only when launch->synchronize is 1. */
 int rt_camera_render_device(rt_camera* cam, const rt_launch* launch, rt_render_stats* stats,
                             uint64_t* work_counters);

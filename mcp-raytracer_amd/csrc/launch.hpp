@@ -15,19 +15,27 @@ struct LaunchGeom {
     int tiles_x;
     int my_tiles;
     int grid;
-    size_t lds_bytes;
+    size_t lds_bytes;  // traversal stack + (lds_scene) the scene blob
+    bool lds_scene;    // copy the scene into LDS (small scenes; never with the reference traversal)
 };
+
+// LDS budget (stack + [tnodes][prims]) up to which the scene is copied into LDS.
+constexpr int kLdsSceneMaxBytes = 152 * 1024;
 
 struct KernelVariant {
     bool emit;   // emission stack (a scattering material emits)
-    bool count;  // work counters
+    int count;   // 0 product, 1 work counters, 2 section timing (diagnostic)
     int trav;    // TRAV_FAST / TRAV_REFERENCE / TRAV_BRUTE (resolved, never AUTO)
 };
 
+// sb == nullptr: the sequential-pixel kernel; else the chunked kernel over sb's pass.
 hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                             const LaunchGeom& g, hipStream_t stream);
+                             const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream);
 hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                              const LaunchGeom& g, hipStream_t stream);
+                              const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream);
+// Per-pixel in-order sum of a chunked pass's sample buffer + outputs + stats.
+hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
+                        const SampleBuf& sb, hipStream_t stream);
 // Resets the stats words / counters / tile counter before a render.
 hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* counters, unsigned int* tile_counter,
                              hipStream_t stream);

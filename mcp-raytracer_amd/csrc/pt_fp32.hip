@@ -4,26 +4,38 @@
 
 namespace rt {
 
-template <bool EMIT, bool COUNT, int TRAV>
-static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
-                     hipStream_t stream) {
-    hipLaunchKernelGGL((pt_render_kernel<float, EMIT, COUNT, TRAV>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
-                       stream, S, reg, out, g.tiles_x, g.my_tiles);
+template <bool EMIT, int INSTR, int TRAV, bool LDSS>
+static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
+                      const SampleBuf* sb, hipStream_t stream) {
+    if (sb)
+        hipLaunchKernelGGL((pt_chunk_kernel<float, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+                           stream, S, reg, out, g.tiles_x, *sb);
+    else
+        hipLaunchKernelGGL((pt_render_kernel<float, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+                           stream, S, reg, out, g.tiles_x, g.my_tiles);
     return hipGetLastError();
+}
+
+template <bool EMIT, int INSTR, int TRAV>
+static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
+                     const SampleBuf* sb, hipStream_t stream) {
+    if (g.lds_scene && TRAV != TRAV_REFERENCE) return go2<EMIT, INSTR, TRAV, TRAV != TRAV_REFERENCE>(S, reg, out, g, sb, stream);
+    return go2<EMIT, INSTR, TRAV, false>(S, reg, out, g, sb, stream);
 }
 
 template <int TRAV>
 static hipError_t go_t(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                       const LaunchGeom& g, hipStream_t stream) {
-    if (v.emit) return v.count ? go<true, true, TRAV>(S, reg, out, g, stream) : go<true, false, TRAV>(S, reg, out, g, stream);
-    return v.count ? go<false, true, TRAV>(S, reg, out, g, stream) : go<false, false, TRAV>(S, reg, out, g, stream);
+                       const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
+    if (v.count == 2) return v.emit ? go<true, 2, TRAV>(S, reg, out, g, sb, stream) : go<false, 2, TRAV>(S, reg, out, g, sb, stream);
+    if (v.count == 1) return v.emit ? go<true, 1, TRAV>(S, reg, out, g, sb, stream) : go<false, 1, TRAV>(S, reg, out, g, sb, stream);
+    return v.emit ? go<true, 0, TRAV>(S, reg, out, g, sb, stream) : go<false, 0, TRAV>(S, reg, out, g, sb, stream);
 }
 
 hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                             const LaunchGeom& g, hipStream_t stream) {
-    if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, stream);
-    if (v.trav == TRAV_FAST) return go_t<TRAV_FAST>(v, S, reg, out, g, stream);
-    return go_t<TRAV_REFERENCE>(v, S, reg, out, g, stream);
+                             const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
+    if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, sb, stream);
+    if (v.trav == TRAV_FAST) return go_t<TRAV_FAST>(v, S, reg, out, g, sb, stream);
+    return go_t<TRAV_REFERENCE>(v, S, reg, out, g, sb, stream);
 }
 
 }  // namespace rt

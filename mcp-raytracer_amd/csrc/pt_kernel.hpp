@@ -32,12 +32,21 @@
 
 namespace rt {
 
+// The scene lives in one device buffer ("blob"): [tnodes][prims][mats][lights][nodes],
+// 16-byte aligned sections. When [tnodes][prims] fits, every workgroup copies
+// it into LDS (LDS-resident launch): traversal and primitive reads are LDS reads.
 struct DevScene {
-    const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
-    const RtNode* __restrict__ fnodes;  // same tree, boxes padded outward (fast traversal)
+    const RtTNode* __restrict__ tnodes; // fast traversal: children-in-parent nodes (blob start)
     const RtPrim* __restrict__ prims;
     const RtMat* __restrict__ mats;
     const RtLight* __restrict__ lights;
+    const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
+    const uint4* __restrict__ blob;     // the whole scene: [tnodes][prims][mats][lights][nodes]
+    int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS ([tnodes][prims])
+    int32_t off_prims;                  // byte offset of prims in the blob
+    int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
+    int32_t troot;                      // fast traversal root reference
+    RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
     double mix_total;  // MixturePDF.totalWeight for [0.5, 0.5/nL x nL]
     double light_w;    // 0.5 / nL
@@ -52,6 +61,13 @@ enum {
     CT_BOUNCES, CT_DIFFUSE, CT_SAMPLES, CT_RAYS, CT_WORDS
 };
 enum : unsigned long long { ERR_NO_BACKGROUND = 1ull, ERR_EMIT_STACK = 2ull };
+// Diagnostic build (INSTR == 2): wave-cycles spent in each section of the path
+// loop (s_memtime, summed over waves), stored after the CT_WORDS counters.
+enum {
+    PR_NEWPATH = 0, PR_RR, PR_HIT, PR_MISS, PR_HITREC, PR_SCATTER, PR_SAMPLE, PR_PDF, PR_ACC, PR_TILE, PR_LOOP,
+    PR_TRIPS, PR_WORDS
+};
+constexpr int kCounterWords = 32;  // CT_WORDS + PR_WORDS, rounded up
 
 struct RenderOut {
     uint8_t* rgb;        // W*H*3 (full frame layout), may be null
@@ -59,7 +75,7 @@ struct RenderOut {
     int32_t* px_samples; // W*H, may be null
     int32_t* px_bounces; // W*H, may be null
     unsigned long long* stats;     // ST_WORDS
-    unsigned long long* counters;  // CT_WORDS (COUNT builds only)
+    unsigned long long* counters;  // kCounterWords (instrumented builds only)
     unsigned int* tile_counter;
 };
 
@@ -68,8 +84,14 @@ struct RenderOut {
 enum Traversal : int32_t { TRAV_FAST = 0, TRAV_REFERENCE = 1, TRAV_BRUTE = 2, TRAV_AUTO = 3 };
 constexpr int kBruteMaxPrims = 16;  // AUTO picks BRUTE up to this many primitives
 
+// Minimum waves per SIMD the path kernel is register-allocated for
+// (__launch_bounds__ second argument): 3 => <= 168 VGPRs.
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 3
+#endif
+
 constexpr int kWave = 64;
-constexpr int kBlock = 256;
+constexpr int kBlock = 768;  // 12 waves = 3 per SIMD: one persistent workgroup per CU shares one LDS scene copy
 constexpr int kTile = 8;          // 8x8 pixels per wave-tile
 constexpr int kEmitStack = 128;   // emission terms kept for the right fold (EMIT builds)
 
@@ -316,7 +338,8 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
 
 constexpr float kTminLo = 0.001f * (1.0f - 1e-5f);
 
-__device__ __forceinline__ bool slab(const RtNode& n, const FRay& f, float thi, float& tnear) {
+template <class R>
+__device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, float& tnear) {
     if (n.bmin[0] != n.bmin[0]) return false;  // box the reference can never enter
     float tn = kTminLo, tf = thi;
 #pragma unroll
@@ -399,6 +422,9 @@ __device__ __forceinline__ float upper_f(Real t) {
 }
 
 // `stk` / `stkt`: this lane's columns of the LDS node / entry-distance stacks.
+// Walks the children-in-parent tree (RtTNode): one 64-byte node read tests
+// both children; the nearer hit child is taken, the farther pushed with its
+// entry distance, and popped entries are culled against the best hit.
 template <class Real, bool COUNT>
 __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
                                                 float* stkt, uint32_t* cnt) {
@@ -408,18 +434,19 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     float thi = __builtin_inff();
     float tn0;
     if (COUNT) cnt[CT_NODE]++;
-    int node = 0;
-    if (!slab(S.fnodes[0], f, thi, tn0)) {
+    if (!slab(S.root_box, f, thi, tn0)) {
         t_hit = best_t;
         return -1;
     }
+    int ref = S.troot;
     int sp = 0;
     while (true) {
-        const RtNode nd = S.fnodes[node];
         bool next = false;
-        if (nd.b < 0) {
-            const int end = nd.a - nd.b;
-            for (int k = nd.a; k < end; ++k) {
+        if (ref < 0) {
+            const int v = ~ref;
+            const int first = v >> 3;
+            const int end = first + (v & 7);
+            for (int k = first; k < end; ++k) {
                 Real t;
                 if (prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt) && (t < best_t || (t == best_t && k < best))) {
                     best_t = t;
@@ -428,19 +455,20 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
                 }
             }
         } else {
+            const RtTNode nd = S.tnodes[ref];
             float ta, tb;
             if (COUNT) cnt[CT_NODE] += 2;
-            const bool ha = slab(S.fnodes[nd.a], f, thi, ta);
-            const bool hb = slab(S.fnodes[nd.b], f, thi, tb);
+            const bool ha = slab(nd.box[0], f, thi, ta);
+            const bool hb = slab(nd.box[1], f, thi, tb);
             if (ha && hb) {
                 const bool a_first = ta <= tb;
-                stk[sp * kBlock] = a_first ? nd.b : nd.a;
+                stk[sp * kBlock] = a_first ? nd.box[1].a : nd.box[0].a;
                 stkt[sp * kBlock] = a_first ? tb : ta;
                 ++sp;
-                node = a_first ? nd.a : nd.b;
+                ref = a_first ? nd.box[0].a : nd.box[1].a;
                 next = true;
             } else if (ha || hb) {
-                node = ha ? nd.a : nd.b;
+                ref = ha ? nd.box[0].a : nd.box[1].a;
                 next = true;
             }
         }
@@ -448,7 +476,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             while (sp > 0) {
                 --sp;
                 if (stkt[sp * kBlock] <= thi) {
-                    node = stk[sp * kBlock];
+                    ref = stk[sp * kBlock];
                     next = true;
                     break;
                 }
@@ -703,12 +731,290 @@ __device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, c
     return closest_hit<Real, COUNT>(S, r, t, stk, cnt);
 }
 
-// Kernel arguments: S must stay the first parameter (cam_opaque reads it at kernarg offset 0).
-template <class Real, bool EMIT, bool COUNT, int TRAV>
-__global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion reg, RenderOut out, int tiles_x,
-                                                           int my_tiles) {
+__device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_memtime(); }
+
+// Diagnostic section timer (INSTR == 2): wave-cycles per path-loop section.
+struct Prof {
+    unsigned long long secs[PR_WORDS];
+    unsigned long long tt, tl;
+};
+template <bool PROF>
+__device__ __forceinline__ void psec(Prof& pf, int k) {
+    if (PROF) {
+        const unsigned long long n = clk();
+        pf.secs[k] += n - pf.tt;
+        pf.tt = n;
+    }
+}
+
+// One path (one rayColor recursion) in flight on a lane.
+template <bool EMIT>
+struct Path {
+    uint64_t rng;
+    V3 o, d, T;
+    int bounces;
+    int em_n;
+    V3 em[EMIT ? kEmitStack : 1];
+};
+
+// Camera.getRay (src/camera.ts:176-210) for sample `sample` of pixel (i, j).
+template <class Real, bool EMIT>
+__device__ __forceinline__ void path_begin(const RtCamera& C, Path<EMIT>& P, int i, int j, uint32_t pix,
+                                           uint32_t sample) {
+    P.rng = rng_init(C.seed, pix, sample);
+    const V3 p00 = ld3(C.pixel00), du = ld3(C.du), dv = ld3(C.dv), cen = ld3(C.center);
+    const V3 pc = add(add(p00, scale<Real>(du, (Real)i)), scale<Real>(dv, (Real)j));
+    V3 ps = pc;
+    if (C.samples > 1.0) {
+        const Real px = (Real)-0.5 + uniform<Real>(P.rng);
+        const Real py = (Real)-0.5 + uniform<Real>(P.rng);
+        ps = add(add(pc, scale<Real>(du, px)), scale<Real>(dv, py));
+    }
+    P.o = cen;
+    P.d = sub(ps, cen);
+    if (C.aperture > 0.0) {
+        V3 rd;
+        while (true) {  // Vec3.randomInUnitDisk (vec3.ts:357-364)
+            const Real a = (Real)2 * uniform<Real>(P.rng) - (Real)1;
+            const Real b = (Real)2 * uniform<Real>(P.rng) - (Real)1;
+            rd = mk<Real>(a, b, (Real)0);
+            if (len2<Real>(rd) < (Real)1) break;
+        }
+        const V3 off = add(scale<Real>(ld3(C.ddu), (Real)rd.x), scale<Real>(ld3(C.ddv), (Real)rd.y));
+        P.o = add(cen, off);
+        P.d = sub(ps, P.o);
+    }
+    P.T = v3(1, 1, 1);
+    P.bounces = 0;
+    P.em_n = 0;
+}
+
+// One level of rayColor (src/camera.ts:221-319). Returns true when the path
+// ends; `c` is then the sample's radiance (the recursion's emitted + ... right
+// fold included).
+template <class Real, bool EMIT, bool COUNT, bool PROF, int TRAV>
+__device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, Path<EMIT>& P, int* stk, float* stkt,
+                                          uint32_t* cnt, unsigned long long& st_err, Prof& pf, V3& c) {
+    bool term = false;
+    c = v3(0, 0, 0);
+    if (P.bounces >= C.depth) {
+        term = true;
+    } else {
+        if (C.roulette && P.bounces >= C.roulette_depth) {
+            const Real mc = js_max<Real>(js_max<Real>((Real)P.T.x, (Real)P.T.y), (Real)P.T.z);
+            const Real p = js_min<Real>(mc, (Real)0.95);
+            if (uniform<Real>(P.rng) > p) term = true;
+            else P.T = divs<Real>(P.T, p);
+        }
+        if (!term) {
+            const RayK<Real> ray = make_ray<Real>(P.o, P.d);
+            Real t;
+            if (COUNT) cnt[CT_RAYS]++;
+            psec<PROF>(pf, PR_RR);
+            const int h = closest_hit_any<Real, COUNT, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
+            psec<PROF>(pf, PR_HIT);
+            if (h < 0) {
+                term = true;
+                if (!C.has_background) st_err |= ERR_NO_BACKGROUND;
+                const V3 ud = unit<Real>(P.d);
+                const Real a = (Real)0.5 * ((Real)ud.y + (Real)1);
+                c = mulv(add(scale<Real>(ld3(C.bg_top), (Real)1 - a), scale<Real>(ld3(C.bg_bottom), a)), P.T);
+                psec<PROF>(pf, PR_MISS);
+            } else {
+                if (COUNT) cnt[CT_MATERIAL]++;
+                // hit record (sphere.ts:67-84, quad.ts:72-83, plane.ts:246-259)
+                const RtPrim pr = S.prims[h];
+                const V3 p = ray_at<Real>(P.o, P.d, t);
+                V3 nrm;
+                bool front;
+                if (pr.type == PRIM_SPHERE) {
+                    nrm = divs<Real>(sub(p, ld3(pr.g0)), sphere_radius<Real>(pr));
+                    front = dot<Real>(P.d, nrm) <= (Real)0;
+                    if (!front) nrm = neg(nrm);
+                } else {
+                    const V3 pn = ld3(pr.g3);
+                    front = dot<Real>(P.d, pn) <= (Real)0;
+                    nrm = front ? pn : neg(pn);
+                }
+                const RtMat hm = S.mats[pr.mat];
+                const V3 emitted = mulv(ld3(hm.emitted), P.T);
+                V3 att, sdir;
+                psec<PROF>(pf, PR_HITREC);
+                const int kind = scatter<Real>(S, pr.mat, P.d, nrm, front, P.rng, att, sdir);
+                psec<PROF>(pf, PR_SCATTER);
+                if (kind == SC_NONE) {
+                    term = true;
+                    c = emitted;
+                } else {
+                    ++P.bounces;
+                    if (kind == SC_SPEC) {
+                        P.T = mulv(P.T, att);
+                        P.o = p;
+                        P.d = sdir;
+                    } else {
+                        if (COUNT) cnt[CT_DIFFUSE]++;
+                        // MixturePDF([CosinePDF(n), light pdfs...], [0.5, 0.5/nL...])
+                        const Onb b = make_onb<Real>(nrm);
+                        const Real total = (Real)S.mix_total;
+                        const Real lw = (Real)S.light_w;
+                        const Real rnd = uniform<Real>(P.rng) * total;
+                        Real partial = (Real)0.5;
+                        V3 gdir;
+                        if (rnd < partial || C.n_lights == 0) {
+                            const Real r1 = uniform<Real>(P.rng);
+                            const Real r2 = uniform<Real>(P.rng);
+                            const Real phi = (Real)2 * K<Real>::PI * r1;
+                            const Real sr2 = m_sqrt(r2);
+                            gdir = onb_local<Real>(b, mk<Real>(m_cos(phi) * sr2, m_sin(phi) * sr2, m_sqrt((Real)1 - r2)));
+                        } else {
+                            int pick = C.n_lights - 1;
+                            for (int l = 0; l < C.n_lights; ++l) {
+                                partial += lw;
+                                if (rnd < partial) { pick = l; break; }
+                            }
+                            gdir = light_generate<Real>(S, S.lights[pick], p, P.rng);
+                        }
+                        psec<PROF>(pf, PR_SAMPLE);
+                        const Real cv = cosine_value<Real>(b, gdir);
+                        Real sum = (Real)0.5 * cv;
+                        for (int l = 0; l < C.n_lights; ++l)
+                            sum += lw * light_pdf_value<Real, COUNT>(S, S.lights[l], p, gdir, cnt);
+                        const Real pv = sum / total;
+                        if (pv <= (Real)0.0001) {
+                            term = true;
+                            c = emitted;
+                        } else {
+                            const V3 brdf = scale<Real>(att, cv);
+                            P.T = divs<Real>(mulv(P.T, brdf), pv);
+                            P.o = p;
+                            P.d = gdir;
+                        }
+                        psec<PROF>(pf, PR_PDF);
+                    }
+                    if (EMIT && !term) {
+                        if (P.em_n < kEmitStack) P.em[P.em_n] = emitted;
+                        else st_err |= ERR_EMIT_STACK;
+                        ++P.em_n;
+                    }
+                }
+            }
+        }
+    }
+    // emitted.add(rayColor(...)) at every level: a right fold.
+    if (EMIT && term) {
+        for (int k = min(P.em_n, kEmitStack) - 1; k >= 0; --k) c = add(P.em[k], c);
+    }
+    return term;
+}
+
+// Per-pixel result: finalColor (src/camera.ts:326-340) + writeColorToBuffer
+// (455-472) + RenderStats.addPixel (renderStats.ts:21-35).
+struct PixStats {
+    unsigned long long pixels = 0, samples = 0, smin = ~0ull, smax = 0, b = 0, bmin = ~0ull, bmax = 0;
+};
+__device__ __forceinline__ void finish_pixel(const RtCamera& C, const RenderOut& out, uint32_t pix, V3 color, int n,
+                                             unsigned long long bsum, int bmin, int bmax, PixStats& st) {
+    V3 fin;
+    if (C.mode == MODE_BOUNCES) {
+        const double avg = n > 0 ? (double)bsum / (double)n : 0.0;
+        fin = mk<double>(0.0, 0.0, js_min<double>(avg / (double)C.depth_raw, 1.0));
+    } else if (C.mode == MODE_SAMPLES) {
+        fin = mk<double>(js_min<double>((double)n / C.samples, 1.0), 0.0, 0.0);
+    } else {
+        fin = divs<double>(color, (double)n);
+    }
+    const size_t off = (size_t)pix * 3;
+    if (out.radiance) {
+        out.radiance[off] = fin.x;
+        out.radiance[off + 1] = fin.y;
+        out.radiance[off + 2] = fin.z;
+    }
+    if (out.rgb) {
+        out.rgb[off] = to_u8(fin.x);
+        out.rgb[off + 1] = to_u8(fin.y);
+        out.rgb[off + 2] = to_u8(fin.z);
+    }
+    if (out.px_samples) out.px_samples[pix] = n;
+    if (out.px_bounces) out.px_bounces[pix] = (int32_t)bsum;
+    st.pixels += 1;
+    st.samples += (unsigned long long)n;
+    st.smin = min(st.smin, (unsigned long long)n);
+    st.smax = max(st.smax, (unsigned long long)n);
+    st.b += bsum;
+    if (n > 0) st.bmin = min(st.bmin, (unsigned long long)bmin);
+    st.bmax = max(st.bmax, (unsigned long long)bmax);
+}
+
+// RenderStats.merge (renderStats.ts:42-64): one atomic per wave.
+__device__ __forceinline__ void publish_stats(const RenderOut& out, const PixStats& st, unsigned long long st_err,
+                                              int lane) {
+    const unsigned long long sp = wave_sum(st.pixels), ss = wave_sum(st.samples), sb = wave_sum(st.b);
+    const unsigned long long smn = wave_min(st.smin), smx = wave_max(st.smax);
+    const unsigned long long bmn = wave_min(st.bmin), bmx = wave_max(st.bmax);
+    unsigned long long err = st_err;
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) err |= __shfl_xor(err, k, 64);
+    if (lane == 0 && sp > 0) {
+        atomicAdd(&out.stats[ST_PIXELS], sp);
+        atomicAdd(&out.stats[ST_SAMPLES], ss);
+        atomicMin(&out.stats[ST_SMIN], smn);
+        atomicMax(&out.stats[ST_SMAX], smx);
+        atomicAdd(&out.stats[ST_BOUNCES], sb);
+        atomicMin(&out.stats[ST_BMIN], bmn);
+        atomicMax(&out.stats[ST_BMAX], bmx);
+    }
+    if (lane == 0 && err) atomicOr(&out.stats[ST_ERROR], err);
+}
+
+template <bool COUNT, bool PROF>
+__device__ __forceinline__ void publish_counters(const RenderOut& out, const uint32_t* cnt, Prof& pf, int lane) {
+    if (COUNT) {
+#pragma unroll
+        for (int k = 0; k < CT_WORDS; ++k) {
+            const unsigned long long v = wave_sum((unsigned long long)cnt[k]);
+            if (lane == 0 && v) atomicAdd(&out.counters[k], v);
+        }
+    }
+    if (PROF) {
+        psec<PROF>(pf, PR_TILE);
+        // s_memtime values are wave-uniform: lane 0 publishes the wave's totals
+#pragma unroll
+        for (int k = 0; k < PR_WORDS; ++k)
+            if (lane == 0) atomicAdd(&out.counters[CT_WORDS + k], pf.secs[k]);
+    }
+}
+
+// Workgroup prologue shared by the render kernels: LDS-resident traversal data
+// (one cooperative copy per workgroup) and this thread's stack columns.
+template <bool LDSS>
+__device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
+    DevScene S = S0;
+    if (LDSS) {
+        uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
+        for (int w = threadIdx.x; w < S0.lds_words; w += kBlock) dst[w] = S0.blob[w];
+        __syncthreads();
+        const char* b = reinterpret_cast<const char*>(dst);
+        S.tnodes = reinterpret_cast<const RtTNode*>(b);
+        S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
+    }
+    return S;
+}
+
+// ---------------------------------------------------------------------------
+// Sequential-pixel kernel (adaptive sampling, and the reference-order
+// traversal): a wave owns an 8x8 tile, lane = pixel, samples in order with
+// per-pixel convergence checks (pixelConverged, src/camera.ts:348-368).
+// Kernel arguments: S0 must stay the first parameter (cam_opaque reads it at kernarg offset 0).
+// INSTR: 0 = product build, 1 = work counters, 2 = section timing.
+// ---------------------------------------------------------------------------
+template <class Real, bool EMIT, int INSTR, int TRAV, bool LDSS>
+__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void pt_render_kernel(DevScene S0, RtRegion reg, RenderOut out,
+                                                                         int tiles_x, int my_tiles) {
+    constexpr bool COUNT = INSTR == 1;
+    constexpr bool PROF = INSTR == 2;
     extern __shared__ int lds_stack[];
-    const RtCamera& C = S.cam;
+    const RtCamera& C = S0.cam;
+    const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
     int* stk = lds_stack + threadIdx.x;
     float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C.stack_depth * kBlock + threadIdx.x;
@@ -721,8 +1027,14 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion 
 #pragma unroll
         for (int k = 0; k < CT_WORDS; ++k) cnt[k] = 0;
     }
-    unsigned long long st_pixels = 0, st_samples = 0, st_smin = ~0ull, st_smax = 0, st_b = 0, st_bmin = ~0ull,
-                       st_bmax = 0, st_err = 0;
+    PixStats st;
+    unsigned long long st_err = 0;
+    Prof pf;
+    if (PROF) {
+#pragma unroll
+        for (int k = 0; k < PR_WORDS; ++k) pf.secs[k] = 0;
+        pf.tt = clk();
+    }
 
     while (true) {
         unsigned int tile = 0;
@@ -743,159 +1055,25 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion 
         int bmin = 0x7fffffff, bmax = 0;
         double sIll = 0.0, sIll2 = 0.0;
 
-        // path state
         bool new_path = true;
-        uint64_t rng = 0;
-        V3 o = v3(0, 0, 0), d = v3(0, 0, 0), T = v3(1, 1, 1);
-        int bounces = 0;
-        V3 em[EMIT ? kEmitStack : 1];
-        int em_n = 0;
-
+        Path<EMIT> P;
+        psec<PROF>(pf, PR_TILE);
         while (active) {
             const RtCamera& C = cam_opaque();
+            if (PROF) { pf.tl = pf.tt; pf.secs[PR_TRIPS]++; }
             if (new_path) {
-                rng = rng_init(C.seed, pix, (uint32_t)n);
-                // getRay (src/camera.ts:176-210)
-                const V3 p00 = ld3(C.pixel00), du = ld3(C.du), dv = ld3(C.dv), cen = ld3(C.center);
-                const V3 pc = add(add(p00, scale<Real>(du, (Real)i)), scale<Real>(dv, (Real)j));
-                V3 ps = pc;
-                if (C.samples > 1.0) {
-                    const Real px = (Real)-0.5 + uniform<Real>(rng);
-                    const Real py = (Real)-0.5 + uniform<Real>(rng);
-                    ps = add(add(pc, scale<Real>(du, px)), scale<Real>(dv, py));
-                }
-                o = cen;
-                d = sub(ps, cen);
-                if (C.aperture > 0.0) {
-                    V3 rd;
-                    while (true) {  // Vec3.randomInUnitDisk (vec3.ts:357-364)
-                        const Real a = (Real)2 * uniform<Real>(rng) - (Real)1;
-                        const Real b = (Real)2 * uniform<Real>(rng) - (Real)1;
-                        rd = mk<Real>(a, b, (Real)0);
-                        if (len2<Real>(rd) < (Real)1) break;
-                    }
-                    const V3 off = add(scale<Real>(ld3(C.ddu), (Real)rd.x), scale<Real>(ld3(C.ddv), (Real)rd.y));
-                    o = add(cen, off);
-                    d = sub(ps, o);
-                }
-                T = v3(1, 1, 1);
-                bounces = 0;
-                em_n = 0;
+                path_begin<Real, EMIT>(C, P, i, j, pix, (uint32_t)n);
                 new_path = false;
+                psec<PROF>(pf, PR_NEWPATH);
             }
-
-            // ---- one rayColor level (src/camera.ts:221-319) ----
-            bool term = false;
-            V3 c = v3(0, 0, 0);
-            if (bounces >= C.depth) {
-                term = true;
-            } else {
-                if (C.roulette && bounces >= C.roulette_depth) {
-                    const Real mc = js_max<Real>(js_max<Real>((Real)T.x, (Real)T.y), (Real)T.z);
-                    const Real p = js_min<Real>(mc, (Real)0.95);
-                    if (uniform<Real>(rng) > p) term = true;
-                    else T = divs<Real>(T, p);
-                }
-                if (!term) {
-                    const RayK<Real> ray = make_ray<Real>(o, d);
-                    Real t;
-                    if (COUNT) cnt[CT_RAYS]++;
-                    const int h = closest_hit_any<Real, COUNT, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
-                    if (h < 0) {
-                        term = true;
-                        if (!C.has_background) st_err |= ERR_NO_BACKGROUND;
-                        const V3 ud = unit<Real>(d);
-                        const Real a = (Real)0.5 * ((Real)ud.y + (Real)1);
-                        c = mulv(add(scale<Real>(ld3(C.bg_top), (Real)1 - a), scale<Real>(ld3(C.bg_bottom), a)), T);
-                    } else {
-                        if (COUNT) cnt[CT_MATERIAL]++;
-                        // hit record (sphere.ts:67-84, quad.ts:72-83, plane.ts:246-259)
-                        const RtPrim pr = S.prims[h];
-                        const V3 p = ray_at<Real>(o, d, t);
-                        V3 nrm;
-                        bool front;
-                        if (pr.type == PRIM_SPHERE) {
-                            nrm = divs<Real>(sub(p, ld3(pr.g0)), sphere_radius<Real>(pr));
-                            front = dot<Real>(d, nrm) <= (Real)0;
-                            if (!front) nrm = neg(nrm);
-                        } else {
-                            const V3 pn = ld3(pr.g3);
-                            front = dot<Real>(d, pn) <= (Real)0;
-                            nrm = front ? pn : neg(pn);
-                        }
-                        const RtMat hm = S.mats[pr.mat];
-                        const V3 emitted = mulv(ld3(hm.emitted), T);
-                        V3 att, sdir;
-                        const int kind = scatter<Real>(S, pr.mat, d, nrm, front, rng, att, sdir);
-                        if (kind == SC_NONE) {
-                            term = true;
-                            c = emitted;
-                        } else {
-                            ++bounces;
-                            if (kind == SC_SPEC) {
-                                T = mulv(T, att);
-                                o = p;
-                                d = sdir;
-                            } else {
-                                if (COUNT) cnt[CT_DIFFUSE]++;
-                                // MixturePDF([CosinePDF(n), light pdfs...], [0.5, 0.5/nL...])
-                                const Onb b = make_onb<Real>(nrm);
-                                const Real total = (Real)S.mix_total;
-                                const Real lw = (Real)S.light_w;
-                                const Real rnd = uniform<Real>(rng) * total;
-                                Real partial = (Real)0.5;
-                                V3 gdir;
-                                if (rnd < partial || C.n_lights == 0) {
-                                    const Real r1 = uniform<Real>(rng);
-                                    const Real r2 = uniform<Real>(rng);
-                                    const Real phi = (Real)2 * K<Real>::PI * r1;
-                                    const Real sr2 = m_sqrt(r2);
-                                    gdir = onb_local<Real>(
-                                        b, mk<Real>(m_cos(phi) * sr2, m_sin(phi) * sr2, m_sqrt((Real)1 - r2)));
-                                } else {
-                                    int pick = C.n_lights - 1;
-                                    for (int l = 0; l < C.n_lights; ++l) {
-                                        partial += lw;
-                                        if (rnd < partial) { pick = l; break; }
-                                    }
-                                    gdir = light_generate<Real>(S, S.lights[pick], p, rng);
-                                }
-                                const Real cv = cosine_value<Real>(b, gdir);
-                                Real sum = (Real)0.5 * cv;
-                                for (int l = 0; l < C.n_lights; ++l)
-                                    sum += lw * light_pdf_value<Real, COUNT>(S, S.lights[l], p, gdir, cnt);
-                                const Real pv = sum / total;
-                                if (pv <= (Real)0.0001) {
-                                    term = true;
-                                    c = emitted;
-                                } else {
-                                    const V3 brdf = scale<Real>(att, cv);
-                                    T = divs<Real>(mulv(T, brdf), pv);
-                                    o = p;
-                                    d = gdir;
-                                }
-                            }
-                            if (EMIT && !term) {
-                                if (em_n < kEmitStack) em[em_n] = emitted;
-                                else st_err |= ERR_EMIT_STACK;
-                                ++em_n;
-                            }
-                        }
-                    }
-                }
-            }
-
-            if (term) {
-                // emitted.add(rayColor(...)) at every level: a right fold.
-                if (EMIT) {
-                    for (int k = min(em_n, kEmitStack) - 1; k >= 0; --k) c = add(em[k], c);
-                }
+            V3 c;
+            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(S, C, P, stk, stkt, cnt, st_err, pf, c)) {
                 // PixelStats.add (renderStats.ts:76-88)
                 color = add(color, c);
                 ++n;
-                bsum += (unsigned long long)bounces;
-                bmin = min(bmin, bounces);
-                bmax = max(bmax, bounces);
+                bsum += (unsigned long long)P.bounces;
+                bmin = min(bmin, P.bounces);
+                bmax = max(bmax, P.bounces);
                 if (C.adaptive) {
                     const double il = illuminance(c);
                     sIll += il;
@@ -903,71 +1081,183 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S, RtRegion 
                 }
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;
-                    cnt[CT_BOUNCES] += (uint32_t)bounces;
+                    cnt[CT_BOUNCES] += (uint32_t)P.bounces;
                 }
                 if (n >= C.n_samples || pixel_converged(C, n, sIll, sIll2)) active = false;
                 else new_path = true;
+                psec<PROF>(pf, PR_ACC);
             }
+            if (PROF) pf.secs[PR_LOOP] += clk() - pf.tl;
         }
-
-        if (valid_px) {
-            // finalColor (src/camera.ts:326-340)
-            V3 fin;
-            if (C.mode == MODE_BOUNCES) {
-                const double avg = n > 0 ? (double)bsum / (double)n : 0.0;
-                fin = mk<double>(0.0, 0.0, js_min<double>(avg / (double)C.depth_raw, 1.0));
-            } else if (C.mode == MODE_SAMPLES) {
-                fin = mk<double>(js_min<double>((double)n / C.samples, 1.0), 0.0, 0.0);
-            } else {
-                fin = divs<double>(color, (double)n);
-            }
-            const size_t off = (size_t)pix * 3;
-            if (out.radiance) {
-                out.radiance[off] = fin.x;
-                out.radiance[off + 1] = fin.y;
-                out.radiance[off + 2] = fin.z;
-            }
-            if (out.rgb) {
-                out.rgb[off] = to_u8(fin.x);
-                out.rgb[off + 1] = to_u8(fin.y);
-                out.rgb[off + 2] = to_u8(fin.z);
-            }
-            if (out.px_samples) out.px_samples[pix] = n;
-            if (out.px_bounces) out.px_bounces[pix] = (int32_t)bsum;
-            st_pixels += 1;
-            st_samples += (unsigned long long)n;
-            st_smin = min(st_smin, (unsigned long long)n);
-            st_smax = max(st_smax, (unsigned long long)n);
-            st_b += bsum;
-            if (n > 0) st_bmin = min(st_bmin, (unsigned long long)bmin);
-            st_bmax = max(st_bmax, (unsigned long long)bmax);
-        }
+        if (valid_px) finish_pixel(C, out, pix, color, n, bsum, bmin, bmax, st);
     }
+    publish_stats(out, st, st_err, lane);
+    publish_counters<COUNT, PROF>(out, cnt, pf, lane);
+}
 
-    // RenderStats.addPixel / merge (renderStats.ts:21-64): one atomic per wave.
-    const unsigned long long sp = wave_sum(st_pixels), ss = wave_sum(st_samples), sb = wave_sum(st_b);
-    const unsigned long long smn = wave_min(st_smin), smx = wave_max(st_smax);
-    const unsigned long long bmn = wave_min(st_bmin), bmx = wave_max(st_bmax);
-    unsigned long long err = st_err;
-#pragma unroll
-    for (int k = 32; k > 0; k >>= 1) err |= __shfl_xor(err, k, 64);
-    if (lane == 0 && sp > 0) {
-        atomicAdd(&out.stats[ST_PIXELS], sp);
-        atomicAdd(&out.stats[ST_SAMPLES], ss);
-        atomicMin(&out.stats[ST_SMIN], smn);
-        atomicMax(&out.stats[ST_SMAX], smx);
-        atomicAdd(&out.stats[ST_BOUNCES], sb);
-        atomicMin(&out.stats[ST_BMIN], bmn);
-        atomicMax(&out.stats[ST_BMAX], bmx);
-    }
-    if (lane == 0 && err) atomicOr(&out.stats[ST_ERROR], err);
+// ---------------------------------------------------------------------------
+// Chunked kernel (fixed spp, no adaptive sampling): the work items are
+// (pixel, chunk of kChunk consecutive samples). Every lane pulls its own items
+// from its wave's pool, which refills 64 items (one tile-chunk) at a time from
+// a global counter - so no lane idles while its wave finishes a tile, and the
+// tail of the launch is one chunk long. Each finished sample's radiance (and
+// bounce count) goes to the sample buffer; pt_accum_kernel then adds every
+// pixel's samples in sample order in fp32, which is exactly PixelStats.add's
+// sequence, so the image is bit-identical to the sequential kernel's.
+// ---------------------------------------------------------------------------
+// Guided schedule: phase p covers samples [s0[p], s0[p] + nch[p] * chunk[p]) in
+// chunks of chunk[p]; items are numbered phase by phase (item_base[p]), and
+// chunks halve from phase to phase, so the launch ends on 1-sample items.
+constexpr int kMaxPhases = 8;
+struct SampleBuf {
+    float4* rec;    // [sample][slot] {r, g, b, bounces (int bits)}
+    int32_t slots;  // pixel slots in this pass = pass_tiles * 64
+    int32_t tile0;  // first of this pass's tiles (index among this launch's tiles)
+    int32_t pool;   // items a wave takes from the global counter at a time (multiple of 64)
+    int32_t n_phases;
+    int32_t n_items;
+    int32_t refill_min;  // idle lanes that trigger a hand-out (all-idle always does)
+    int32_t s0[kMaxPhases], chunk[kMaxPhases], nch[kMaxPhases], item_base[kMaxPhases];
+    double rnch[kMaxPhases];  // 1.0 / nch
+};
+
+// n / d for 0 <= n < 2^31, d >= 1, through a double reciprocal (rinv = 1.0 / d)
+// and one correction step: cheaper than the integer division sequence.
+__device__ __forceinline__ int udiv(int n, int d, double rinv) {
+    int q = (int)((double)n * rinv);
+    const int r = n - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return q;
+}
+
+__device__ __forceinline__ void item_pixel(const RtRegion& reg, int tiles_x, int mt, int l, int& i, int& j) {
+    const int gt = reg.tile_group + mt * reg.tile_groups;
+    const int ty = gt / tiles_x;
+    i = reg.x + (gt - ty * tiles_x) * kTile + (l & (kTile - 1));
+    j = reg.y + ty * kTile + (l / kTile);
+}
+__device__ __forceinline__ void item_pixel(const RtRegion& reg, int tiles_x, double rtx, int mt, int l, int& i,
+                                           int& j) {
+    const int gt = reg.tile_group + mt * reg.tile_groups;
+    const int ty = udiv(gt, tiles_x, rtx);
+    i = reg.x + (gt - ty * tiles_x) * kTile + (l & (kTile - 1));
+    j = reg.y + ty * kTile + (l / kTile);
+}
+
+template <class Real, bool EMIT, int INSTR, int TRAV, bool LDSS>
+__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void pt_chunk_kernel(DevScene S0, RtRegion reg, RenderOut out,
+                                                                        int tiles_x, SampleBuf sb) {
+    constexpr bool COUNT = INSTR == 1;
+    constexpr bool PROF = INSTR == 2;
+    extern __shared__ int lds_stack[];
+    const RtCamera& C0 = S0.cam;
+    const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
+    const int lane = threadIdx.x & (kWave - 1);
+    int* stk = lds_stack + threadIdx.x;
+    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kBlock + threadIdx.x;
+    const int endX = min(reg.x + reg.width, C0.width);
+    const int endY = min(reg.y + reg.height, C0.height);
+    const int n_items = sb.n_items;
+
+    uint32_t cnt[CT_WORDS];
     if (COUNT) {
 #pragma unroll
-        for (int k = 0; k < CT_WORDS; ++k) {
-            const unsigned long long v = wave_sum((unsigned long long)cnt[k]);
-            if (lane == 0 && v) atomicAdd(&out.counters[k], v);
+        for (int k = 0; k < CT_WORDS; ++k) cnt[k] = 0;
+    }
+    unsigned long long st_err = 0;
+    Prof pf;
+    if (PROF) {
+#pragma unroll
+        for (int k = 0; k < PR_WORDS; ++k) pf.secs[k] = 0;
+        pf.tt = clk();
+    }
+
+    int pool_next = 0, pool_end = 0;  // wave-uniform
+    bool exhausted = false;           // wave-uniform
+    int slot = -1;                    // this lane's pixel slot (-1: idle)
+    int s = 0, s_end = 0, i = 0, j = 0;
+    uint32_t pix = 0;
+    bool new_path = false;
+    Path<EMIT> P;
+    const double rtx = 1.0 / (double)tiles_x;
+
+    while (true) {
+        // hand out items to idle lanes (wave-uniform control flow); waits until
+        // refill_min lanes are idle so the hand-out cost is shared
+        const unsigned long long need = __ballot(slot < 0);
+        const int n_need = __popcll(need);
+        if (n_need != 0 && !exhausted && (n_need >= sb.refill_min || __ballot(slot >= 0) == 0ull)) {
+            if (pool_next >= pool_end) {
+                int base = 0;
+                if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
+                base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+                if (base >= n_items) {
+                    exhausted = true;
+                } else {
+                    pool_next = base;
+                    pool_end = min(base + sb.pool, n_items);
+                }
+            }
+            if (!exhausted) {
+                const int take = min(n_need, pool_end - pool_next);
+                const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                if (slot < 0 && rank < take) {
+                    const int u = pool_next + rank;
+                    int ph = 0;
+                    for (int k = 1; k < sb.n_phases; ++k)
+                        if (u >= sb.item_base[k]) ph = k;
+                    const int v = u - sb.item_base[ph];  // item within the phase: (tile, chunk) groups of 64
+                    const int q = v >> 6, l = v & 63;
+                    const int tl = udiv(q, sb.nch[ph], sb.rnch[ph]), ch = q - tl * sb.nch[ph];
+                    item_pixel(reg, tiles_x, rtx, sb.tile0 + tl, l, i, j);
+                    if (i < endX && j < endY) {
+                        slot = tl * 64 + l;
+                        s = sb.s0[ph] + ch * sb.chunk[ph];
+                        s_end = s + sb.chunk[ph];
+                        pix = (uint32_t)j * (uint32_t)C0.width + (uint32_t)i;
+                        new_path = true;
+                    }
+                }
+                pool_next += take;
+            }
+        }
+        if (__ballot(slot >= 0) == 0ull) {
+            if (exhausted) break;
+            continue;
+        }
+        if (slot >= 0) {
+            const RtCamera& C = cam_opaque();
+            if (PROF) { pf.tl = pf.tt; pf.secs[PR_TRIPS]++; }
+            if (new_path) {
+                path_begin<Real, EMIT>(C, P, i, j, pix, (uint32_t)s);
+                new_path = false;
+            }
+            psec<PROF>(pf, PR_NEWPATH);
+            V3 c;
+            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(S, C, P, stk, stkt, cnt, st_err, pf, c)) {
+                float4 r;
+                r.x = c.x;
+                r.y = c.y;
+                r.z = c.z;
+                r.w = __int_as_float(P.bounces);
+                sb.rec[(size_t)s * sb.slots + slot] = r;
+                if (COUNT) {
+                    cnt[CT_SAMPLES]++;
+                    cnt[CT_BOUNCES] += (uint32_t)P.bounces;
+                }
+                ++s;
+                if (s < s_end) new_path = true;
+                else slot = -1;
+                psec<PROF>(pf, PR_ACC);
+            }
+            if (PROF) pf.secs[PR_LOOP] += clk() - pf.tl;
         }
     }
+    PixStats st;
+    publish_stats(out, st, st_err, lane);
+    publish_counters<COUNT, PROF>(out, cnt, pf, lane);
 }
 
 }  // namespace rt

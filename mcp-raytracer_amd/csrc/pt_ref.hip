@@ -5,34 +5,100 @@
 
 namespace rt {
 
-template <bool EMIT, bool COUNT, int TRAV>
-static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
-                     hipStream_t stream) {
-    hipLaunchKernelGGL((pt_render_kernel<double, EMIT, COUNT, TRAV>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
-                       stream, S, reg, out, g.tiles_x, g.my_tiles);
+template <bool EMIT, int INSTR, int TRAV, bool LDSS>
+static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
+                      const SampleBuf* sb, hipStream_t stream) {
+    if (sb)
+        hipLaunchKernelGGL((pt_chunk_kernel<double, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+                           stream, S, reg, out, g.tiles_x, *sb);
+    else
+        hipLaunchKernelGGL((pt_render_kernel<double, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+                           stream, S, reg, out, g.tiles_x, g.my_tiles);
     return hipGetLastError();
+}
+
+template <bool EMIT, int INSTR, int TRAV>
+static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
+                     const SampleBuf* sb, hipStream_t stream) {
+    if (g.lds_scene && TRAV != TRAV_REFERENCE) return go2<EMIT, INSTR, TRAV, TRAV != TRAV_REFERENCE>(S, reg, out, g, sb, stream);
+    return go2<EMIT, INSTR, TRAV, false>(S, reg, out, g, sb, stream);
 }
 
 template <int TRAV>
 static hipError_t go_t(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                       const LaunchGeom& g, hipStream_t stream) {
-    if (v.emit) return v.count ? go<true, true, TRAV>(S, reg, out, g, stream) : go<true, false, TRAV>(S, reg, out, g, stream);
-    return v.count ? go<false, true, TRAV>(S, reg, out, g, stream) : go<false, false, TRAV>(S, reg, out, g, stream);
+                       const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
+    if (v.count == 2) return v.emit ? go<true, 2, TRAV>(S, reg, out, g, sb, stream) : go<false, 2, TRAV>(S, reg, out, g, sb, stream);
+    if (v.count == 1) return v.emit ? go<true, 1, TRAV>(S, reg, out, g, sb, stream) : go<false, 1, TRAV>(S, reg, out, g, sb, stream);
+    return v.emit ? go<true, 0, TRAV>(S, reg, out, g, sb, stream) : go<false, 0, TRAV>(S, reg, out, g, sb, stream);
 }
 
 hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                             const LaunchGeom& g, hipStream_t stream) {
-    if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, stream);
-    if (v.trav == TRAV_FAST) return go_t<TRAV_FAST>(v, S, reg, out, g, stream);
-    return go_t<TRAV_REFERENCE>(v, S, reg, out, g, stream);
+                             const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
+    if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, sb, stream);
+    if (v.trav == TRAV_FAST) return go_t<TRAV_FAST>(v, S, reg, out, g, sb, stream);
+    return go_t<TRAV_REFERENCE>(v, S, reg, out, g, sb, stream);
 }
 
 __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long* counters,
                                   unsigned int* tile_counter) {
     const int t = threadIdx.x;
     if (t < ST_WORDS) stats[t] = (t == ST_SMIN || t == ST_BMIN) ? ~0ull : 0ull;
-    if (counters && t < CT_WORDS) counters[t] = 0ull;
+    if (counters && t < kCounterWords) counters[t] = 0ull;
     if (t == 0) *tile_counter = 0u;
+}
+
+// Adds every pixel's samples in sample order (PixelStats.add), then
+// finalColor / u8 / RenderStats exactly as the sequential kernel.
+__global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
+                                                        SampleBuf sb) {
+    const RtCamera& C = S0.cam;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    PixStats st;
+    if (slot < sb.slots) {
+        int i, j;
+        item_pixel(reg, tiles_x, sb.tile0 + slot / 64, slot % 64, i, j);
+        if (i < min(reg.x + reg.width, C.width) && j < min(reg.y + reg.height, C.height)) {
+            V3 color = v3(0, 0, 0);
+            unsigned long long bsum = 0;
+            int bmin = 0x7fffffff, bmax = 0;
+            const int n = C.n_samples;
+            // records are [sample][slot] (coalesced across the wave); 8 loads in flight
+            const float4* rec = sb.rec + slot;
+            const size_t stride = (size_t)sb.slots;
+            int k = 0;
+            for (; k + 8 <= n; k += 8) {
+                float4 r[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) r[m] = rec[(size_t)(k + m) * stride];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    color = add(color, v3(r[m].x, r[m].y, r[m].z));
+                    const int b = __float_as_int(r[m].w);
+                    bsum += (unsigned long long)b;
+                    bmin = min(bmin, b);
+                    bmax = max(bmax, b);
+                }
+            }
+            for (; k < n; ++k) {
+                const float4 r = rec[(size_t)k * stride];
+                color = add(color, v3(r.x, r.y, r.z));
+                const int b = __float_as_int(r.w);
+                bsum += (unsigned long long)b;
+                bmin = min(bmin, b);
+                bmax = max(bmax, b);
+            }
+            finish_pixel(C, out, (uint32_t)j * (uint32_t)C.width + (uint32_t)i, color, n, bsum, bmin, bmax, st);
+        }
+    }
+    publish_stats(out, st, 0ull, lane);
+}
+
+hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
+                        const SampleBuf& sb, hipStream_t stream) {
+    const int grid = (sb.slots + 255) / 256;
+    hipLaunchKernelGGL(pt_accum_kernel, dim3(grid), dim3(256), 0, stream, S, reg, out, tiles_x, sb);
+    return hipGetLastError();
 }
 
 hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* counters, unsigned int* tile_counter,

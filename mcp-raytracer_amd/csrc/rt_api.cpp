@@ -26,6 +26,19 @@ namespace {
 
 thread_local std::string g_error;
 
+// A/B switches for measurements: RT_AMD_LDS_SCENE=0 (no LDS-resident scene),
+// RT_AMD_CHUNKED=0 (sequential-pixel kernel for fixed-spp renders).
+bool env_flag(const char* name, bool dflt) {
+    const char* e = std::getenv(name);
+    if (!e || !e[0]) return dflt;
+    return e[0] != '0';
+}
+bool lds_scene_enabled() { return env_flag("RT_AMD_LDS_SCENE", true); }
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return (e && e[0]) ? std::max(1, std::atoi(e)) : dflt;
+}
+
 int set_error(int code, const std::string& msg) {
     g_error = msg;
     return code;
@@ -55,11 +68,10 @@ struct rt_camera {
     std::mutex mu;
 
     int device = -1;
-    RtNode* d_nodes = nullptr;
-    RtNode* d_fnodes = nullptr;
-    RtPrim* d_prims = nullptr;
-    RtMat* d_mats = nullptr;
-    RtLight* d_lights = nullptr;
+    uint4* d_blob = nullptr;  // [tnodes][prims][mats][lights][nodes] (DevScene)
+    int32_t lds_words = 0;    // [tnodes][prims] prefix, 16-byte words
+    int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0;
+    int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     unsigned long long* d_stats = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned int* d_tile = nullptr;
@@ -74,20 +86,21 @@ struct rt_camera {
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
-        for (void* p : {(void*)d_nodes, (void*)d_fnodes, (void*)d_prims, (void*)d_mats, (void*)d_lights, (void*)d_stats,
-                        (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad})
+        for (void* p : {(void*)d_blob, (void*)d_stats, (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad,
+                        (void*)d_sbuf})
             if (p) (void)hipFree(p);
+        d_sbuf = nullptr;
+        sbuf_cap = 0;
         (void)hipSetDevice(prev);
         device = -1;
     }
 
     template <class T>
-    static T* upload(const std::vector<T>& v) {
-        T* p = nullptr;
-        const size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(T);
-        hip_check(hipMalloc(&p, bytes), "hipMalloc");
-        if (!v.empty()) hip_check(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
-        return p;
+    static void append(std::vector<char>& blob, const std::vector<T>& v, int32_t* off) {
+        static_assert(sizeof(T) % 16 == 0, "scene records are 16-byte multiples");
+        if (off) *off = (int32_t)blob.size();
+        const char* p = reinterpret_cast<const char*>(v.data());
+        blob.insert(blob.end(), p, p + v.size() * sizeof(T));
     }
 
     void ensure_device() {
@@ -95,16 +108,23 @@ struct rt_camera {
         hip_check(hipGetDevice(&dev), "hipGetDevice");
         if (device == dev) return;
         if (device >= 0) release();
-        d_nodes = upload(build.nodes);
-        d_fnodes = upload(build.fnodes);
-        d_prims = upload(build.prims);
-        d_mats = upload(build.mats);
-        d_lights = upload(build.lights);
+        std::vector<char> blob;
+        append(blob, build.tnodes, nullptr);
+        append(blob, build.prims, &off_prims);
+        lds_words = (int32_t)(blob.size() / 16);
+        append(blob, build.mats, &off_mats);
+        append(blob, build.lights, &off_lights);
+        append(blob, build.nodes, &off_nodes);
+        hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
+        if (!blob.empty()) hip_check(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice), "hipMemcpy");
         hip_check(hipMalloc(&d_stats, ST_WORDS * sizeof(unsigned long long)), "hipMalloc");
-        hip_check(hipMalloc(&d_counters, CT_WORDS * sizeof(unsigned long long)), "hipMalloc");
+        hip_check(hipMalloc(&d_counters, kCounterWords * sizeof(unsigned long long)), "hipMalloc");
         hip_check(hipMalloc(&d_tile, 64), "hipMalloc");
         device = dev;
         cus = device_cus(dev);
+        int smem = 0;
+        if (hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && smem > 0)
+            lds_max = smem;
     }
 
     void ensure_frame() {
@@ -124,11 +144,18 @@ struct rt_camera {
 
     DevScene dev_scene() const {
         DevScene S;
-        S.nodes = d_nodes;
-        S.fnodes = d_fnodes;
-        S.prims = d_prims;
-        S.mats = d_mats;
-        S.lights = d_lights;
+        const char* b = reinterpret_cast<const char*>(d_blob);
+        S.tnodes = reinterpret_cast<const RtTNode*>(b);
+        S.prims = reinterpret_cast<const RtPrim*>(b + off_prims);
+        S.mats = reinterpret_cast<const RtMat*>(b + off_mats);
+        S.lights = reinterpret_cast<const RtLight*>(b + off_lights);
+        S.nodes = reinterpret_cast<const RtNode*>(b + off_nodes);
+        S.blob = d_blob;
+        S.lds_words = lds_words;
+        S.off_prims = off_prims;
+        S.lds_stack_bytes = 0;
+        S.troot = build.troot;
+        S.root_box = build.fnodes.empty() ? RtNode{} : build.fnodes[0];
         S.cam = build.cam;
         S.mix_total = mix_total;
         S.light_w = light_w;
@@ -136,7 +163,7 @@ struct rt_camera {
     }
 
     // Launch one render; returns after queueing (and synchronising if asked).
-    void launch(const rt_region& region, int tile_group, int tile_groups, int prec, int trav, bool count,
+    void launch(const rt_region& region, int tile_group, int tile_groups, int prec, int trav, int count,
                 uint8_t* rgb, float* rad, int32_t* pxs, int32_t* pxb, hipStream_t stream) {
         const RtCamera& C = build.cam;
         if (tile_groups < 1 || tile_group < 0 || tile_group >= tile_groups)
@@ -153,27 +180,118 @@ struct rt_camera {
         g.tiles_x = std::max(tiles_x, 1);
         g.my_tiles = (int)mine;
         const long want = (mine + (kBlock / kWave) - 1) / (kBlock / kWave);
-        g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus * 8));
+        g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus));  // one persistent workgroup per CU
         const KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
-        g.lds_bytes = stack_lds_bytes(C.stack_depth, v.trav);
+        const size_t stack = stack_lds_bytes(C.stack_depth, v.trav);
+        g.lds_scene = lds_scene_enabled() && v.trav != TRAV_REFERENCE &&
+                      stack + (size_t)lds_words * 16 <= (size_t)std::min(lds_max, kLdsSceneMaxBytes);
+        g.lds_bytes = stack + (g.lds_scene ? (size_t)lds_words * 16 : 0);
+        if (g.lds_bytes > (size_t)lds_max)
+            throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
         if (mine == 0) return;
-        const DevScene S = dev_scene();
-        hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, g, stream)
-                                         : launch_render_ref(v, S, reg, out, g, stream);
-        hip_check(e, "pt_render_kernel launch");
+        DevScene S = dev_scene();
+        S.lds_stack_bytes = (int32_t)stack;
+        // Fixed spp: the chunked kernel balances small images (few tiles per
+        // resident wave) far better; large images already balance over tiles and
+        // skip the sample-buffer round trip.
+        const long resident_waves = (long)cus * (kBlock / kWave);
+        const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 8 * resident_waves);
+        if (C.adaptive || C.n_samples <= 0 || !chunked) {
+            // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
+            hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, g, nullptr, stream)
+                                             : launch_render_ref(v, S, reg, out, g, nullptr, stream);
+            hip_check(e, "pt_render_kernel launch");
+            return;
+        }
+        // chunked kernel: passes over at most sbuf_budget bytes of per-sample records
+        const size_t rec_per_tile = (size_t)kWave * (size_t)C.n_samples * sizeof(float4);
+        const long pass_tiles = std::max<long>(1, std::min<long>(mine, (long)(sbuf_budget() / rec_per_tile)));
+        ensure_sbuf((size_t)pass_tiles * rec_per_tile);
+        SampleBuf sb{};
+        sb.rec = d_sbuf;
+        sb.pool = kWave * env_int("RT_AMD_POOL", 1);
+        // guided schedule: half of the remaining samples per phase, chunks halving
+        {
+            int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", 16), std::max(1, C.n_samples / 2)), np = 0;
+            if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
+                c = std::min(env_int("RT_AMD_CHUNK", 16), C.n_samples);
+                const int full = C.n_samples / c;
+                sb.s0[np] = 0; sb.chunk[np] = c; sb.nch[np] = full; ++np;
+                s0 = full * c;
+            }
+            while (s0 < C.n_samples) {
+                const int rem = C.n_samples - s0;
+                if (c <= 1 || np == kMaxPhases - 1) {  // final phase: 1-sample items
+                    sb.s0[np] = s0; sb.chunk[np] = 1; sb.nch[np] = rem;
+                    ++np;
+                    break;
+                }
+                const int span = (rem / 2) / c * c;
+                if (span == 0) { c /= 2; continue; }
+                sb.s0[np] = s0; sb.chunk[np] = c; sb.nch[np] = span / c;
+                ++np;
+                s0 += span;
+                c /= 2;
+            }
+            sb.n_phases = np;
+            int covered = 0;
+            for (int p = 0; p < np; ++p) {
+                if (sb.s0[p] != covered) throw std::runtime_error("guided schedule: gap");
+                covered += sb.chunk[p] * sb.nch[p];
+            }
+            if (covered != C.n_samples) throw std::runtime_error("guided schedule: coverage");
+            for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
+            sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
+        }
+        for (long t0 = 0; t0 < mine; t0 += pass_tiles) {
+            const long nt = std::min(pass_tiles, mine - t0);
+            sb.tile0 = (int32_t)t0;
+            sb.slots = (int32_t)(nt * kWave);
+            long items = 0;
+            for (int p = 0; p < sb.n_phases; ++p) {
+                sb.item_base[p] = (int32_t)items;
+                items += (long)sb.slots * sb.nch[p];
+            }
+            if (items >= (1l << 31) - 4096) throw std::runtime_error("chunked pass too large");
+            sb.n_items = (int32_t)items;
+            if (t0 > 0) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
+            LaunchGeom gp = g;
+            gp.grid = (int)std::max<long>(1, std::min<long>(items / kBlock + 1, (long)cus));
+            hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, gp, &sb, stream)
+                                             : launch_render_ref(v, S, reg, out, gp, &sb, stream);
+            hip_check(e, "pt_chunk_kernel launch");
+            hip_check(launch_accum(S, reg, out, g.tiles_x, sb, stream), "pt_accum_kernel launch");
+        }
+    }
+
+    // Per-sample record buffer of the chunked kernel (grown on demand, kept).
+    float4* d_sbuf = nullptr;
+    size_t sbuf_cap = 0;
+    void ensure_sbuf(size_t bytes) {
+        if (bytes <= sbuf_cap) return;
+        if (d_sbuf) (void)hipFree(d_sbuf);
+        d_sbuf = nullptr;
+        sbuf_cap = 0;
+        hip_check(hipMalloc(&d_sbuf, bytes), "hipMalloc(sample buffer)");
+        sbuf_cap = bytes;
+    }
+    static size_t sbuf_budget() {
+        const char* e = std::getenv("RT_AMD_SBUF_MB");
+        const long mb = e ? std::atol(e) : 8192;
+        return (size_t)std::max<long>(mb, 1) << 20;
     }
 
     void read_stats(rt_render_stats* st, uint64_t* counters, hipStream_t stream) {
         unsigned long long w[ST_WORDS];
         hip_check(hipMemcpyAsync(w, d_stats, sizeof w, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
-        unsigned long long c[CT_WORDS];
+        unsigned long long c[kCounterWords];
         if (counters)
             hip_check(hipMemcpyAsync(c, d_counters, sizeof c, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
         hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
         if (counters)
-            for (int k = 0; k < CT_WORDS; ++k) counters[k] = c[k];
+            for (int k = 0; k < kCounterWords; ++k) counters[k] = c[k];
         if (w[ST_ERROR] & ERR_NO_BACKGROUND)
             throw std::runtime_error("Cannot read properties of undefined (reading 'top')");
         if (w[ST_ERROR] & ERR_EMIT_STACK)
@@ -320,7 +438,7 @@ int rt_camera_render_region(rt_camera* cam, const rt_region* region, uint8_t* rg
         cam->ensure_frame();
         const RtCamera& C = cam->build.cam;
         const hipStream_t stream = nullptr;
-        cam->launch(*region, 0, 1, cam->precision, cam->traversal, false, rgb ? cam->d_rgb : nullptr,
+        cam->launch(*region, 0, 1, cam->precision, cam->traversal, 0, rgb ? cam->d_rgb : nullptr,
                     radiance ? cam->d_rad : nullptr, nullptr, nullptr, stream);
         cam->read_stats(stats, nullptr, stream);
         // copy back only the region's rows/columns (the caller's buffer is the full frame)
@@ -363,7 +481,8 @@ int rt_camera_render_device(rt_camera* cam, const rt_launch* L, rt_render_stats*
         const hipStream_t stream = (hipStream_t)L->stream;
         const int prec = L->precision < 0 ? cam->precision : L->precision;
         const int trav = L->traversal < 0 ? cam->traversal : L->traversal;
-        cam->launch(L->region, L->tile_group, L->tile_groups, prec, trav, L->count_work != 0, L->rgb, L->radiance,
+        if (L->count_work < 0 || L->count_work > 2) throw std::invalid_argument("count_work must be 0, 1 or 2");
+        cam->launch(L->region, L->tile_group, L->tile_groups, prec, trav, L->count_work, L->rgb, L->radiance,
                     L->px_samples, L->px_bounces, stream);
         if (L->synchronize) cam->read_stats(stats, L->count_work ? work_counters : nullptr, stream);
         return RT_OK;

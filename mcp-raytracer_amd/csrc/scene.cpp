@@ -713,6 +713,11 @@ struct Builder {
             p.g2[0] = v.x; p.g2[1] = v.y; p.g2[2] = v.z;
             p.g3[0] = n.x; p.g3[1] = n.y; p.g3[2] = n.z;
             p.g4[0] = w.x; p.g4[1] = w.y; p.g4[2] = w.z;
+            // |w||u| and |w||v| (rounded up) bound alpha/beta's sensitivity in the
+            // kernel's fp32 interval test (pt_kernel.hpp planar_ival)
+            const double wn = std::sqrt(len2<double>(w));
+            p.g1[3] = (float)(wn * std::sqrt(len2<double>(u)) * (1.0 + 1e-5));
+            p.g2[3] = (float)(wn * std::sqrt(len2<double>(v)) * (1.0 + 1e-5));
             if (p.type == PRIM_PLANE) {
                 const double eps = 1e-4;
                 if (std::fabs((double)n.x) > 0.9999) {
@@ -861,6 +866,34 @@ std::vector<RtNode> make_fast_nodes(const std::vector<RtNode>& nodes) {
             }
         }
     }
+    return out;
+}
+
+// fnodes (DFS order, node 0 = root) re-laid out as RtTNode: interior nodes get
+// TNode slots in DFS order and carry both children's boxes.
+std::vector<RtTNode> make_tnodes(const std::vector<RtNode>& f, int32_t& root_ref) {
+    std::vector<int32_t> tidx(f.size(), -1);
+    int32_t nt = 0;
+    for (size_t i = 0; i < f.size(); ++i)
+        if (f[i].b >= 0) tidx[i] = nt++;
+    auto ref = [&](int32_t i) -> int32_t {
+        if (f[i].b >= 0) return tidx[i];
+        const int32_t count = -f[i].b;
+        if (count < 1 || count > 7 || f[i].a >= (1 << 27)) throw std::runtime_error("BVH leaf does not fit the TNode code");
+        return ~((f[i].a << 3) | count);
+    };
+    std::vector<RtTNode> out((size_t)nt);
+    for (size_t i = 0; i < f.size(); ++i) {
+        if (f[i].b < 0) continue;
+        RtTNode& t = out[(size_t)tidx[i]];
+        const int32_t ch[2] = {f[i].a, f[i].b};
+        for (int k = 0; k < 2; ++k) {
+            t.box[k] = f[(size_t)ch[k]];
+            t.box[k].a = ref(ch[k]);
+            t.box[k].b = 0;
+        }
+    }
+    root_ref = f.empty() ? ~0 : ref(0);
     return out;
 }
 
@@ -1052,6 +1085,7 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
     cam.seed = (uint32_t)(int64_t)seed;
     cam.stack_depth = b.out.bvh_depth + 1;
     b.out.fnodes = make_fast_nodes(b.out.nodes);
+    b.out.tnodes = make_tnodes(b.out.fnodes, b.out.troot);
     b.out.fast_ok = prims_inside_boxes(b.out.prims);
     return std::move(b.out);
 }

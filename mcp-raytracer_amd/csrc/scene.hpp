@@ -45,13 +45,22 @@ struct alignas(16) RtNode {
 };
 static_assert(sizeof(RtNode) == 32, "RtNode must be 32 bytes");
 
+// Fast-traversal node: the boxes of BOTH children live in the parent, so one
+// 64-byte fetch tests two children. box[k] uses the RtNode box layout (padded
+// fnodes boxes) and box[k].a is the child reference: >= 0 another RtTNode,
+// < 0 a leaf ~((first_prim << 3) | count).
+struct alignas(16) RtTNode {
+    RtNode box[2];
+};
+static_assert(sizeof(RtTNode) == 64, "RtTNode must be 64 bytes");
+
 struct alignas(16) RtPrim {
     int32_t type;
     int32_t mat;
     double s0;     // sphere: radius (JS double); quad/plane: D = normal·Q (double)
     float g0[4];   // sphere: center.xyz, (float)radius | quad/plane: Q.xyz, (float)D
-    float g1[4];   // quad/plane: u.xyz, -
-    float g2[4];   // quad/plane: v.xyz, -
+    float g1[4];   // quad/plane: u.xyz, |w||u| (rounded up)
+    float g2[4];   // quad/plane: v.xyz, |w||v| (rounded up)
     float g3[4];   // quad/plane: normal.xyz, -
     float g4[4];   // quad/plane: w.xyz, -
 };
@@ -120,6 +129,8 @@ struct RtRegion {
 struct SceneBuild {
     std::vector<RtNode> nodes;
     std::vector<RtNode> fnodes;  // same tree, boxes for the fast traversal (padded / reject-marked)
+    std::vector<RtTNode> tnodes; // fnodes re-laid out children-in-parent (fast traversal)
+    int32_t troot = 0;           // reference of the root (TNode index or leaf code)
     std::vector<RtPrim> prims;
     std::vector<RtMat> mats;
     std::vector<RtLight> lights;

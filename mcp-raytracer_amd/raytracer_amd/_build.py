@@ -46,17 +46,20 @@ def _newest_input() -> float:
     return max(p.stat().st_mtime for p in paths)
 
 
-def build_native(force: bool = False, verbose: bool = False) -> Path:
-    """Compile (if stale) and return the path of librt_amd.so."""
-    if not force and LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= _newest_input():
-        return LIB_PATH
+def build_native(force: bool = False, verbose: bool = False, variant: str = "", defines=()) -> Path:
+    """Compile (if stale) and return the path of librt_amd.so. `variant` + `defines`
+    build an experimental lib/librt_amd_<variant>.so (loaded with RT_AMD_VARIANT)."""
+    lib_path = LIB_PATH.with_name(f"librt_amd_{variant}.so") if variant else LIB_PATH
+    if not force and lib_path.exists() and lib_path.stat().st_mtime >= _newest_input():
+        return lib_path
     cc = hipcc()
-    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    obj_dir = OBJ_DIR / variant if variant else OBJ_DIR
+    obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     objs = []
     for src, flags, is_hip in _UNITS:
-        obj = OBJ_DIR / (src.replace(".", "_") + ".o")
-        cmd = [cc, *_COMMON, *flags]
+        obj = obj_dir / (src.replace(".", "_") + ".o")
+        cmd = [cc, *_COMMON, *flags, *[f"-D{d}" for d in defines]]
         if is_hip:
             cmd.append(f"--offload-arch={ARCH}")
         cmd += ["-c", str(CSRC / src), "-o", str(obj)]
@@ -64,14 +67,19 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         objs.append(str(obj))
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    tmp = lib_path.with_suffix(".so.tmp")
     cmd = [cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build_native(force=True, verbose=True))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    print(build_native(force=True, verbose=True, variant=a.variant, defines=a.defines))

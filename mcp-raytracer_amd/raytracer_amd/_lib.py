@@ -22,6 +22,8 @@ TRAVERSAL = {"fast": 0, "reference": 1, "brute": 2, "auto": 3}
 
 CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_sphere",
             "bounces", "diffuse", "samples", "rays"]
+PR_NAMES = ["newpath", "rr", "hit", "miss", "hitrec", "scatter", "sample", "pdf", "acc", "tile", "loop", "trips"]
+COUNTER_WORDS = 32
 
 
 class RtRegion(C.Structure):
@@ -92,8 +94,14 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
-        raise ImportError(f"librt_amd.so not found at {LIB_PATH}; run __graft_entry__.build() "
+    path = LIB_PATH
+    variant = os.environ.get("RT_AMD_VARIANT")  # experiments: lib/librt_amd_<variant>.so (same package dir)
+    if variant:
+        if not variant.isidentifier():
+            raise ImportError(f"bad RT_AMD_VARIANT {variant!r}")
+        path = LIB_PATH.with_name(f"librt_amd_{variant}.so")
+    if not path.exists():
+        raise ImportError(f"{path.name} not found at {path}; run __graft_entry__.build() "
                           "(hipcc --offload-arch=gfx950) first - there is no CPU fallback")
     # PyTorch-ROCm ships its own libamdhip64.so.7 (same soname as /opt/rocm's).
     # Whichever loads first serves the whole process, and torch cannot run on a
@@ -103,7 +111,7 @@ def load() -> C.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    lib = C.CDLL(os.fspath(LIB_PATH))
+    lib = C.CDLL(os.fspath(path))
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype = res

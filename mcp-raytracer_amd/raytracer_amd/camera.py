@@ -157,7 +157,8 @@ class Camera:
         L.tile_group, L.tile_groups = int(tile_group), int(tile_groups)
         L.precision = -1 if precision is None else _lib.PRECISION[precision]
         L.traversal = -1 if traversal is None else _lib.TRAVERSAL[traversal]
-        L.count_work = 1 if count_work else 0
+        # count_work: False/True (work counters) or "profile" (section timing, diagnostic)
+        L.count_work = 2 if count_work == "profile" else (1 if count_work else 0)
         L.rgb = rgb_ptr
         L.radiance = radiance_ptr
         L.px_samples = px_samples_ptr
@@ -165,11 +166,15 @@ class Camera:
         L.stream = stream
         L.synchronize = 1 if synchronize else 0
         st = _lib.RtRenderStats()
-        cnt = (C.c_uint64 * len(_lib.CT_NAMES))()
+        cnt = (C.c_uint64 * _lib.COUNTER_WORDS)()
         _lib.check(self._lib.rt_camera_render_device(self._h, C.byref(L), C.byref(st), cnt))
         if not synchronize:
             return None, None
-        counters = dict(zip(_lib.CT_NAMES, [int(v) for v in cnt])) if count_work else None
+        if count_work == "profile":
+            base = len(_lib.CT_NAMES)
+            counters = {k: int(cnt[base + i]) for i, k in enumerate(_lib.PR_NAMES)}
+        else:
+            counters = dict(zip(_lib.CT_NAMES, [int(v) for v in cnt])) if count_work else None
         return RenderStats._from_c(st), counters
 
     # -- introspection (tests) -----------------------------------------------
