@@ -156,6 +156,12 @@ int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint
 /* Number of visible HIP devices (0 without a GPU). */
 int rt_device_count(int32_t* count);
 
+/* Device time of the most recent rt_camera_render_device / render_region call,
+ * from HIP events recorded on its stream: `path_ms` = the path-tracing
+ * kernel(s), `accum_ms` = the chunked mode's in-order accumulate pass (0 for the
+ * sequential kernel). Waits for that call's events. */
+int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms);
+
 #ifdef __cplusplus
 }
 #endif

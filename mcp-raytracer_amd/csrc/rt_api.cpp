@@ -72,6 +72,8 @@ struct rt_camera {
     int32_t lds_words = 0;    // [tnodes][prims] prefix, 16-byte words
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // path start, path end, accumulate end
+    bool ev_recorded = false, ev_accum = false;
     unsigned long long* d_stats = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned int* d_tile = nullptr;
@@ -89,6 +91,9 @@ struct rt_camera {
         for (void* p : {(void*)d_blob, (void*)d_stats, (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad,
                         (void*)d_sbuf})
             if (p) (void)hipFree(p);
+        for (hipEvent_t& e : ev)
+            if (e) (void)hipEventDestroy(e), e = nullptr;
+        ev_recorded = false;
         d_sbuf = nullptr;
         sbuf_cap = 0;
         (void)hipSetDevice(prev);
@@ -122,6 +127,7 @@ struct rt_camera {
         hip_check(hipMalloc(&d_tile, 64), "hipMalloc");
         device = dev;
         cus = device_cus(dev);
+        for (hipEvent_t& e : ev) hip_check(hipEventCreate(&e), "hipEventCreate");
         int smem = 0;
         if (hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && smem > 0)
             lds_max = smem;
@@ -190,6 +196,7 @@ struct rt_camera {
             throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
+        ev_recorded = false;
         if (mine == 0) return;
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
@@ -200,9 +207,13 @@ struct rt_camera {
         const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 8 * resident_waves);
         if (C.adaptive || C.n_samples <= 0 || !chunked) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
+            hip_check(hipEventRecord(ev[0], stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, g, nullptr, stream)
                                              : launch_render_ref(v, S, reg, out, g, nullptr, stream);
             hip_check(e, "pt_render_kernel launch");
+            hip_check(hipEventRecord(ev[1], stream), "hipEventRecord");
+            ev_recorded = true;
+            ev_accum = false;
             return;
         }
         // chunked kernel: passes over at most sbuf_budget bytes of per-sample records
@@ -259,11 +270,16 @@ struct rt_camera {
             if (t0 > 0) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = g;
             gp.grid = (int)std::max<long>(1, std::min<long>(items / kBlock + 1, (long)cus));
+            if (t0 == 0) hip_check(hipEventRecord(ev[0], stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, gp, &sb, stream)
                                              : launch_render_ref(v, S, reg, out, gp, &sb, stream);
             hip_check(e, "pt_chunk_kernel launch");
+            if (t0 + pass_tiles >= mine) hip_check(hipEventRecord(ev[1], stream), "hipEventRecord");
             hip_check(launch_accum(S, reg, out, g.tiles_x, sb, stream), "pt_accum_kernel launch");
         }
+        hip_check(hipEventRecord(ev[2], stream), "hipEventRecord");
+        ev_recorded = true;
+        ev_accum = true;
     }
 
     // Per-sample record buffer of the chunked kernel (grown on demand, kept).
@@ -549,6 +565,25 @@ int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint
         out[k] = (xs >> rot) | (xs << ((32u - rot) & 31u));
     }
     return RT_OK;
+}
+
+int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms) {
+    if (!cam || !path_ms || !accum_ms) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    try {
+        *path_ms = 0.0f;
+        *accum_ms = 0.0f;
+        if (!cam->ev_recorded) return RT_OK;
+        hip_check(hipEventSynchronize(cam->ev[1]), "hipEventSynchronize");
+        hip_check(hipEventElapsedTime(path_ms, cam->ev[0], cam->ev[1]), "hipEventElapsedTime");
+        if (cam->ev_accum) {
+            hip_check(hipEventSynchronize(cam->ev[2]), "hipEventSynchronize");
+            hip_check(hipEventElapsedTime(accum_ms, cam->ev[1], cam->ev[2]), "hipEventElapsedTime");
+        }
+        return RT_OK;
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_DEVICE, e.what());
+    }
 }
 
 int rt_device_count(int32_t* count) {

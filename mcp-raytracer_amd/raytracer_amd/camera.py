@@ -177,6 +177,12 @@ class Camera:
             counters = dict(zip(_lib.CT_NAMES, [int(v) for v in cnt])) if count_work else None
         return RenderStats._from_c(st), counters
 
+    def kernel_times(self):
+        """(path_ms, accum_ms) of the last render call, from HIP events on its stream."""
+        a, b = C.c_float(), C.c_float()
+        _lib.check(self._lib.rt_camera_kernel_times(self._h, C.byref(a), C.byref(b)))
+        return float(a.value), float(b.value)
+
     # -- introspection (tests) -----------------------------------------------
     def export(self):
         """Host copies of the flattened scene as numpy structured arrays."""
