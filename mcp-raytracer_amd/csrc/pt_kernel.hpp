@@ -37,7 +37,8 @@ namespace rt {
 // it into LDS (LDS-resident launch): traversal and primitive reads are LDS reads.
 struct DevScene {
     const RtTNode* __restrict__ tnodes; // fast traversal: children-in-parent nodes (blob start)
-    const RtPrim* __restrict__ prims;
+    const RtPrim* __restrict__ prims;   // global, or LDS in an LDS-resident launch
+    const RtPrim* __restrict__ gprims;  // always the global copy (scalar-load reads)
     const RtMat* __restrict__ mats;
     const RtLight* __restrict__ lights;
     const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
@@ -155,6 +156,21 @@ template <class Real> struct K {
 
 __device__ __forceinline__ V3 ld3(const float* p) { return V3{p[0], p[1], p[2]}; }
 
+// Wave-uniform reads of scene records that are never written during a launch:
+// through the constant address space, so the compiler emits scalar loads
+// (s_load, scalar cache) instead of vector loads with full memory latency.
+template <class T>
+__device__ __forceinline__ T ld_uniform(const T* base, int k) {
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    typedef const __attribute__((address_space(4))) uint32_t* CW;
+    const CW src = (CW)(const void*)(base + k);
+    T out;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
+    return out;
+}
+
 // Per-ray constants reused by every node and primitive test.
 template <class Real> struct RayK {
     V3 o, d;
@@ -239,6 +255,85 @@ __device__ __forceinline__ bool planar_t(const RtPrim& p, const RayK<Real>& r, R
     t = tt;
     return true;
 }
+
+constexpr float kTminLo = 0.001f * (1.0f - 1e-5f);  // below the reference's tMin with margin (fp32 tests)
+
+// Axis-aligned quad (scene.cpp encode_axis_quad): Plane.intersect + Quad's
+// alpha/beta test with the terms that are exact zeros dropped. Every kept
+// operation is the reference's own (a product of two fp32 values is exact in
+// double, x - (+-0) = x, sums with +-0 are exact), so t and the accept/reject
+// decision are bit-identical to planar_t - provided no 0*inf/NaN term would
+// have turned the reference's result into NaN, which the finiteness guard
+// reproduces (a non-finite off-axis ray component makes the reference miss).
+// One specialisation per axis code (constant indices: no selects, no branches).
+template <class Real, int CODE>
+__device__ __forceinline__ bool aquad_t_c(const RtPrim& p, V3 o3, V3 d3, Real tmin, Real tmax, Real& t) {
+    constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
+    constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+    const float o[3] = {o3.x, o3.y, o3.z}, d[3] = {d3.x, d3.y, d3.z};
+    if (!(::isfinite(o[ia]) && ::isfinite(d[ia]) && ::isfinite(o[ib]) && ::isfinite(d[ib]))) return false;
+    const Real na = (Real)p.g3[a];
+    const Real denom = na * (Real)d[a];
+    if (m_abs(denom) < (Real)1e-8) return false;
+    const Real tt = (plane_d<Real>(p) - na * (Real)o[a]) / denom;
+    if (!(tmin < tt && tt < tmax)) return false;
+    // Ray.at(t) in-plane components, hit point minus Q (fp32 stores)
+    const float ph1 = (o[ia] + (float)((Real)d[ia] * tt)) - p.g0[ia];
+    const float ph2 = (o[ib] + (float)((Real)d[ib] * tt)) - p.g0[ib];
+    const Real sw = (Real)p.g3[3];
+    const Real alpha = sw * (Real)(ph1 * p.g2[3]);
+    const Real beta = sw * (Real)(ph2 * p.g1[3]);
+    if (alpha < (Real)0 || alpha > (Real)1 || beta < (Real)0 || beta > (Real)1) return false;
+    t = tt;
+    return true;
+}
+
+// fp32 pre-filter of aquad_t_c: false only when the exact test surely rejects or
+// gives no t <= thi.
+template <int CODE>
+__device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, const float* d, float sa, float thi) {
+    constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
+    constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+    const float na = p.g3[a];
+    const float denom = na * d[a];
+    if (!(::fabsf(denom) > 1e-6f * sa)) return true;  // near-parallel: decide exactly
+    const float no = na * o[a];
+    const float D = p.g0[3];
+    const float t = (D - no) / denom;
+    const float et = 1e-4f * (::fabsf(D) + ::fabsf(no)) / ::fabsf(denom) + 1e-30f;
+    if (t + et < kTminLo || t - et > thi) return false;
+    const float ph1 = o[ia] + t * d[ia] - p.g0[ia];
+    const float ph2 = o[ib] + t * d[ib] - p.g0[ib];
+    const float alpha = p.g3[3] * (ph1 * p.g2[3]);
+    const float beta = p.g3[3] * (ph2 * p.g1[3]);
+    const float ea = 1e-3f;
+    return !(alpha < -ea || alpha > 1.0f + ea || beta < -ea || beta > 1.0f + ea);
+}
+
+template <class Real>
+__device__ __forceinline__ bool aquad_t(const RtPrim& p, int code, V3 o, V3 d, Real tmin, Real tmax, Real& t) {
+    switch (code) {
+        case 1: return aquad_t_c<Real, 1>(p, o, d, tmin, tmax, t);
+        case 2: return aquad_t_c<Real, 2>(p, o, d, tmin, tmax, t);
+        case 3: return aquad_t_c<Real, 3>(p, o, d, tmin, tmax, t);
+        case 4: return aquad_t_c<Real, 4>(p, o, d, tmin, tmax, t);
+        case 5: return aquad_t_c<Real, 5>(p, o, d, tmin, tmax, t);
+        default: return aquad_t_c<Real, 6>(p, o, d, tmin, tmax, t);
+    }
+}
+__device__ __forceinline__ bool aquad_maybe(const RtPrim& p, int code, const float* o, const float* d, float a2,
+                                            float thi) {
+    const float sa = ::sqrtf(a2);
+    switch (code) {
+        case 1: return aquad_maybe_c<1>(p, o, d, sa, thi);
+        case 2: return aquad_maybe_c<2>(p, o, d, sa, thi);
+        case 3: return aquad_maybe_c<3>(p, o, d, sa, thi);
+        case 4: return aquad_maybe_c<4>(p, o, d, sa, thi);
+        case 5: return aquad_maybe_c<5>(p, o, d, sa, thi);
+        default: return aquad_maybe_c<6>(p, o, d, sa, thi);
+    }
+}
+__device__ __forceinline__ int aquad_code(const RtPrim& p) { return __float_as_int(p.g4[3]); }
 
 template <class Real, bool COUNT>
 __device__ __forceinline__ bool prim_t(const RtPrim& p, const RayK<Real>& r, Real tmin, Real tmax, Real& t,
@@ -336,7 +431,6 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
     return f;
 }
 
-constexpr float kTminLo = 0.001f * (1.0f - 1e-5f);
 
 template <class R>
 __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, float& tnear) {
@@ -406,6 +500,11 @@ __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>
     }
     if (p.type == PRIM_QUAD) {
         if (COUNT) cnt[CT_QUAD]++;
+        const int code = aquad_code(p);
+        if (code != 0) {
+            if (!aquad_maybe(p, code, f.o, f.d, f.a, thi)) return false;
+            return aquad_t<Real>(p, code, r.o, r.d, K<Real>::TMIN, inf, t);
+        }
         if (!planar_maybe<true>(p, f, thi)) return false;
         return planar_t<Real, true>(p, r, K<Real>::TMIN, inf, t);
     }
@@ -502,7 +601,8 @@ __device__ __forceinline__ int closest_hit_brute(const DevScene& S, int n_prims,
     float thi = __builtin_inff();
     for (int k = 0; k < n_prims; ++k) {
         Real t;
-        if (prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt) && t < best_t) {
+        const RtPrim p = ld_uniform(S.gprims, k);
+        if (prim_candidate<Real, COUNT>(p, r, f, thi, t, cnt) && t < best_t) {
             best_t = t;
             best = k;
             thi = upper_f<Real>(t);
@@ -618,15 +718,18 @@ __device__ __forceinline__ int scatter(const DevScene& S, int mi, V3 din, V3 n, 
 
 // Quad.pdfValue / Sphere.pdfValue (quad.ts:123-140, sphere.ts:106-131):
 // re-intersect the light on (0.001, inf), not occlusion-aware.
-template <class Real, bool COUNT>
+template <class Real, bool COUNT, bool UNIFORM = false>
 __device__ __forceinline__ Real light_pdf_value(const DevScene& S, const RtLight& L, V3 origin, V3 dir,
                                                 uint32_t* cnt) {
-    const RtPrim p = S.prims[L.prim];
+    const RtPrim p = UNIFORM ? ld_uniform(S.gprims, L.prim) : S.prims[L.prim];
     const RayK<Real> r = make_ray<Real>(origin, dir);
     Real t;
     if (L.type == PRIM_QUAD) {
         if (COUNT) cnt[CT_LIGHT_QUAD]++;
-        if (!planar_t<Real, true>(p, r, K<Real>::TMIN, (Real)__builtin_inf(), t)) return (Real)0;
+        const int code = aquad_code(p);
+        const bool hit = code != 0 ? aquad_t<Real>(p, code, origin, dir, K<Real>::TMIN, (Real)__builtin_inf(), t)
+                                   : planar_t<Real, true>(p, r, K<Real>::TMIN, (Real)__builtin_inf(), t);
+        if (!hit) return (Real)0;
         const V3 hp = ray_at<Real>(origin, dir, t);
         const V3 n = ld3(p.g3);
         const bool front = dot<Real>(dir, n) <= (Real)0;
@@ -872,13 +975,13 @@ __device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, 
                                 partial += lw;
                                 if (rnd < partial) { pick = l; break; }
                             }
-                            gdir = light_generate<Real>(S, S.lights[pick], p, P.rng);
+                            gdir = light_generate<Real>(S, S.lights[pick], p, P.rng);  // pick: per lane
                         }
                         psec<PROF>(pf, PR_SAMPLE);
                         const Real cv = cosine_value<Real>(b, gdir);
                         Real sum = (Real)0.5 * cv;
                         for (int l = 0; l < C.n_lights; ++l)
-                            sum += lw * light_pdf_value<Real, COUNT>(S, S.lights[l], p, gdir, cnt);
+                            sum += lw * light_pdf_value<Real, COUNT, true>(S, ld_uniform(S.lights, l), p, gdir, cnt);
                         const Real pv = sum / total;
                         if (pv <= (Real)0.0001) {
                             term = true;

@@ -153,6 +153,7 @@ struct rt_camera {
         const char* b = reinterpret_cast<const char*>(d_blob);
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.prims = reinterpret_cast<const RtPrim*>(b + off_prims);
+        S.gprims = S.prims;
         S.mats = reinterpret_cast<const RtMat*>(b + off_mats);
         S.lights = reinterpret_cast<const RtLight*>(b + off_lights);
         S.nodes = reinterpret_cast<const RtNode*>(b + off_nodes);
@@ -189,7 +190,10 @@ struct rt_camera {
         g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus));  // one persistent workgroup per CU
         const KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
         const size_t stack = stack_lds_bytes(C.stack_depth, v.trav);
-        g.lds_scene = lds_scene_enabled() && v.trav != TRAV_REFERENCE &&
+        // LDS copy for the BVH walk only: the brute-force loop reads its (wave-
+        // uniform) primitive records through scalar loads, which keeps the
+        // per-primitive control flow scalar.
+        g.lds_scene = lds_scene_enabled() && v.trav == TRAV_FAST &&
                       stack + (size_t)lds_words * 16 <= (size_t)std::min(lds_max, kLdsSceneMaxBytes);
         g.lds_bytes = stack + (g.lds_scene ? (size_t)lds_words * 16 : 0);
         if (g.lds_bytes > (size_t)lds_max)

@@ -681,6 +681,35 @@ struct Builder {
 
     // Plane ctor (src/entities/plane.ts:180-200) + boxes (plane.ts:276-308,
     // quad.ts:400-422); Sphere ctor (sphere.ts:20-31).
+    // Axis-aligned quad (u, v each along one axis): the kernel evaluates the
+    // reference's Plane.intersect / alpha / beta with the zero terms dropped,
+    // which rounds identically (pt_kernel.hpp aquad_t). Encoding:
+    //   g4[3] = int code 1 + a + 3*vflag (a = normal axis; vflag: v along (a+2)%3),
+    //   g3[3] = +-w[a] (sign folded from the cross product), g2[3] = v's nonzero
+    //   component, g1[3] = u's nonzero component. code 0 = general quad.
+    static void encode_axis_quad(RtPrim& p, V3 u, V3 v, V3 cp, V3 w) {
+        const float uu[3] = {u.x, u.y, u.z}, vv[3] = {v.x, v.y, v.z}, cc[3] = {cp.x, cp.y, cp.z},
+                    ww[3] = {w.x, w.y, w.z};
+        auto only = [](const float* x) {
+            int k = -1;
+            for (int i = 0; i < 3; ++i) {
+                if (!std::isfinite(x[i])) return -2;
+                if (x[i] != 0.0f) k = (k == -1) ? i : -2;
+            }
+            return k;
+        };
+        const int iu = only(uu), iv = only(vv), a = only(cc), iw = only(ww);
+        if (iu < 0 || iv < 0 || a < 0 || iw != a || iu == iv || iu == a || iv == a) return;
+        const int b = (a + 1) % 3, c = (a + 2) % 3;
+        const bool vflag = iv == c;  // then u is along b
+        if (!(vflag ? iu == b : (iv == b && iu == c))) return;
+        int32_t code = 1 + a + 3 * (vflag ? 1 : 0);
+        std::memcpy(&p.g4[3], &code, sizeof code);
+        p.g3[3] = vflag ? ww[a] : -ww[a];
+        p.g2[3] = vv[iv];
+        p.g1[3] = uu[iu];
+    }
+
     RtPrim make_prim(const Value& od, int mat, Box& box, std::string& type_out) {
         RtPrim p{};
         p.mat = mat;
@@ -713,11 +742,7 @@ struct Builder {
             p.g2[0] = v.x; p.g2[1] = v.y; p.g2[2] = v.z;
             p.g3[0] = n.x; p.g3[1] = n.y; p.g3[2] = n.z;
             p.g4[0] = w.x; p.g4[1] = w.y; p.g4[2] = w.z;
-            // |w||u| and |w||v| (rounded up) bound alpha/beta's sensitivity in the
-            // kernel's fp32 interval test (pt_kernel.hpp planar_ival)
-            const double wn = std::sqrt(len2<double>(w));
-            p.g1[3] = (float)(wn * std::sqrt(len2<double>(u)) * (1.0 + 1e-5));
-            p.g2[3] = (float)(wn * std::sqrt(len2<double>(v)) * (1.0 + 1e-5));
+            if (p.type == PRIM_QUAD) encode_axis_quad(p, u, v, cp, w);
             if (p.type == PRIM_PLANE) {
                 const double eps = 1e-4;
                 if (std::fabs((double)n.x) > 0.9999) {

@@ -59,10 +59,10 @@ struct alignas(16) RtPrim {
     int32_t mat;
     double s0;     // sphere: radius (JS double); quad/plane: D = normal·Q (double)
     float g0[4];   // sphere: center.xyz, (float)radius | quad/plane: Q.xyz, (float)D
-    float g1[4];   // quad/plane: u.xyz, |w||u| (rounded up)
-    float g2[4];   // quad/plane: v.xyz, |w||v| (rounded up)
-    float g3[4];   // quad/plane: normal.xyz, -
-    float g4[4];   // quad/plane: w.xyz, -
+    float g1[4];   // quad/plane: u.xyz, axis quad: u's nonzero component
+    float g2[4];   // quad/plane: v.xyz, axis quad: v's nonzero component
+    float g3[4];   // quad/plane: normal.xyz, axis quad: +-w[a]
+    float g4[4];   // quad/plane: w.xyz, quad: axis code (int bits, 0 = general; scene.cpp encode_axis_quad)
 };
 static_assert(sizeof(RtPrim) == 96, "RtPrim must be 96 bytes");
 
