@@ -257,6 +257,12 @@ __device__ __forceinline__ bool planar_t(const RtPrim& p, const RayK<Real>& r, R
 }
 
 constexpr float kTminLo = 0.001f * (1.0f - 1e-5f);  // below the reference's tMin with margin (fp32 tests)
+// fp32 pre-filter error model: every estimate below is an fp32 evaluation of the
+// reference's fp64 formula, off by at most a few tens of ulps of the operand
+// magnitudes (products of fp32 values are exact in fp64). kRel (~170 ulps)
+// bounds that with a wide margin; the margins scale with |o|, |d|, |Q|, r so
+// they hold for any scene scale. Hardware rcp/sqrt (<= 1 ulp) are inside kRel.
+constexpr float kRel = 1e-5f;
 
 // Axis-aligned quad (scene.cpp encode_axis_quad): Plane.intersect + Quad's
 // alpha/beta test with the terms that are exact zeros dropped. Every kept
@@ -291,23 +297,28 @@ __device__ __forceinline__ bool aquad_t_c(const RtPrim& p, V3 o3, V3 d3, Real tm
 // fp32 pre-filter of aquad_t_c: false only when the exact test surely rejects or
 // gives no t <= thi.
 template <int CODE>
-__device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, const float* d, float sa, float thi) {
+__device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, const float* d, float dn, float thi) {
     constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
     constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
     const float na = p.g3[a];
     const float denom = na * d[a];
-    if (!(::fabsf(denom) > 1e-6f * sa)) return true;  // near-parallel: decide exactly
+    if (!(::fabsf(denom) > 1e-3f * dn)) return true;  // near-parallel: decide exactly
     const float no = na * o[a];
     const float D = p.g0[3];
-    const float t = (D - no) / denom;
-    const float et = 1e-4f * (::fabsf(D) + ::fabsf(no)) / ::fabsf(denom) + 1e-30f;
+    const float idn = __builtin_amdgcn_rcpf(denom);
+    const float t = (D - no) * idn;
+    const float et = kRel * ((::fabsf(D) + ::fabsf(no)) * ::fabsf(idn) + 2.0f * ::fabsf(t)) + 1e-30f;
     if (t + et < kTminLo || t - et > thi) return false;
     const float ph1 = o[ia] + t * d[ia] - p.g0[ia];
     const float ph2 = o[ib] + t * d[ib] - p.g0[ib];
     const float alpha = p.g3[3] * (ph1 * p.g2[3]);
     const float beta = p.g3[3] * (ph2 * p.g1[3]);
-    const float ea = 1e-3f;
-    return !(alpha < -ea || alpha > 1.0f + ea || beta < -ea || beta > 1.0f + ea);
+    // in-plane hit-point error, times |w_a v| (alpha) / |w_a u| (beta)
+    const float dp1 = et * ::fabsf(d[ia]) + kRel * (::fabsf(o[ia]) + ::fabsf(t * d[ia]) + ::fabsf(p.g0[ia]));
+    const float dp2 = et * ::fabsf(d[ib]) + kRel * (::fabsf(o[ib]) + ::fabsf(t * d[ib]) + ::fabsf(p.g0[ib]));
+    const float ea = ::fabsf(p.g3[3] * p.g2[3]) * dp1 + 1e-4f;
+    const float eb = ::fabsf(p.g3[3] * p.g1[3]) * dp2 + 1e-4f;
+    return !(alpha < -ea || alpha > 1.0f + ea || beta < -eb || beta > 1.0f + eb);
 }
 
 template <class Real>
@@ -321,16 +332,15 @@ __device__ __forceinline__ bool aquad_t(const RtPrim& p, int code, V3 o, V3 d, R
         default: return aquad_t_c<Real, 6>(p, o, d, tmin, tmax, t);
     }
 }
-__device__ __forceinline__ bool aquad_maybe(const RtPrim& p, int code, const float* o, const float* d, float a2,
+__device__ __forceinline__ bool aquad_maybe(const RtPrim& p, int code, const float* o, const float* d, float dn,
                                             float thi) {
-    const float sa = ::sqrtf(a2);
     switch (code) {
-        case 1: return aquad_maybe_c<1>(p, o, d, sa, thi);
-        case 2: return aquad_maybe_c<2>(p, o, d, sa, thi);
-        case 3: return aquad_maybe_c<3>(p, o, d, sa, thi);
-        case 4: return aquad_maybe_c<4>(p, o, d, sa, thi);
-        case 5: return aquad_maybe_c<5>(p, o, d, sa, thi);
-        default: return aquad_maybe_c<6>(p, o, d, sa, thi);
+        case 1: return aquad_maybe_c<1>(p, o, d, dn, thi);
+        case 2: return aquad_maybe_c<2>(p, o, d, dn, thi);
+        case 3: return aquad_maybe_c<3>(p, o, d, dn, thi);
+        case 4: return aquad_maybe_c<4>(p, o, d, dn, thi);
+        case 5: return aquad_maybe_c<5>(p, o, d, dn, thi);
+        default: return aquad_maybe_c<6>(p, o, d, dn, thi);
     }
 }
 __device__ __forceinline__ int aquad_code(const RtPrim& p) { return __float_as_int(p.g4[3]); }
@@ -415,7 +425,12 @@ struct FRay {
     float d[3];
     float inv[3];  // 1/d with zero components replaced by +-1e-30 (no 0*inf NaNs)
     float a;       // |d|^2
+    float ia;      // ~1/|d|^2
+    float on;      // |o| (rounded up)
+    float dn;      // |d| (rounded up)
 };
+
+
 
 __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
     FRay f;
@@ -428,6 +443,9 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
         f.inv[a] = 1.0f / cc;
     }
     f.a = d.x * d.x + d.y * d.y + d.z * d.z;
+    f.ia = __builtin_amdgcn_rcpf(f.a);
+    f.dn = __builtin_amdgcn_sqrtf(f.a) * (1.0f + kRel);
+    f.on = __builtin_amdgcn_sqrtf(o.x * o.x + o.y * o.y + o.z * o.z) * (1.0f + kRel);
     return f;
 }
 
@@ -449,17 +467,19 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 
 // fp32 pre-filters: false only when the exact test surely gives no t <= thi.
 __device__ __forceinline__ bool sphere_maybe(const RtPrim& p, const FRay& f, float thi) {
-    const float ox = f.o[0] - p.g0[0], oy = f.o[1] - p.g0[1], oz = f.o[2] - p.g0[2];
+    const float ox = f.o[0] - p.g0[0], oy = f.o[1] - p.g0[1], oz = f.o[2] - p.g0[2];  // = the reference's oc
     const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
     const float r = p.g0[3];
-    const float c = (ox * ox + oy * oy + oz * oz) - r * r;
-    const float disc = b * b - f.a * c;
-    const float tol = 1e-4f * (b * b + ::fabsf(f.a * c)) + 1e-30f;
+    const float oo = ox * ox + oy * oy + oz * oz;
+    const float disc = b * b - f.a * (oo - r * r);
+    // every term of disc is bounded by a*(|oc|^2 + r^2) (b^2 <= a|oc|^2); the
+    // bound holds through the cancellation of |oc|^2 - r^2 for rays leaving the surface
+    const float tol = 4.0f * kRel * f.a * (oo + r * r) + 1e-30f;
     if (disc < -tol) return false;
-    const float sq = ::sqrtf(::fmaxf(disc, 0.0f) + tol);
-    const float et = 1e-4f * (::fabsf(b) + sq) / f.a;
-    if ((-b + sq) / f.a + et < kTminLo) return false;
-    if ((-b - sq) / f.a - et > thi) return false;
+    const float sq = __builtin_amdgcn_sqrtf(::fmaxf(disc, 0.0f) + tol) * (1.0f + kRel);
+    const float et = kRel * (__builtin_amdgcn_sqrtf(oo * f.a) + ::fabsf(b) + sq) * f.ia + 1e-30f;
+    if ((-b + sq) * f.ia * (1.0f + kRel) + et < kTminLo) return false;
+    if ((-b - sq) * f.ia * (1.0f - kRel) - et > thi) return false;
     return true;
 }
 
@@ -467,11 +487,14 @@ template <bool QUAD>
 __device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, float thi) {
     const float nx = p.g3[0], ny = p.g3[1], nz = p.g3[2];
     const float denom = nx * f.d[0] + ny * f.d[1] + nz * f.d[2];
-    if (!(::fabsf(denom) > 1e-6f * ::sqrtf(f.a))) return true;  // near-parallel: decide exactly
+    if (!(::fabsf(denom) > 1e-3f * f.dn)) return true;  // near-parallel: decide exactly
     const float no = nx * f.o[0] + ny * f.o[1] + nz * f.o[2];
     const float D = p.g0[3];
-    const float t = (D - no) / denom;
-    const float et = 1e-4f * (::fabsf(D) + ::fabsf(no)) / ::fabsf(denom) + 1e-30f;
+    const float idn = __builtin_amdgcn_rcpf(denom);
+    const float t = (D - no) * idn;
+    // |n| = 1: num error <= kRel(|D| + |o|), denominator error <= kRel|d| (< 1% of |denom|)
+    const float et = (kRel * (::fabsf(D) + f.on) + 2.0f * kRel * f.dn * ::fabsf(t)) * ::fabsf(idn) +
+                     kRel * ::fabsf(t) + 1e-30f;
     if (t + et < kTminLo || t - et > thi) return false;
     if (!QUAD) return true;
     const float px = f.o[0] + t * f.d[0] - p.g0[0];
@@ -483,8 +506,11 @@ __device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, flo
     // alpha = w . (ph x v), beta = w . (u x ph)
     const float alpha = wx * (py * vz - pz * vy) + wy * (pz * vx - px * vz) + wz * (px * vy - py * vx);
     const float beta = wx * (uy * pz - uz * py) + wy * (uz * px - ux * pz) + wz * (ux * py - uy * px);
-    const float ea = 1e-3f;
-    if (alpha < -ea || alpha > 1.0f + ea || beta < -ea || beta > 1.0f + ea) return false;
+    // hit-point error (t error, Ray.at's and ph's roundings) times |w||v| / |w||u| (scene.cpp)
+    const float dp = et * f.dn + kRel * (f.on + ::fabsf(t) * f.dn + ::fabsf(p.g0[0]) + ::fabsf(p.g0[1]) +
+                                         ::fabsf(p.g0[2]) + ::fabsf(px) + ::fabsf(py) + ::fabsf(pz));
+    const float ea = p.g2[3] * dp + 1e-4f, eb = p.g1[3] * dp + 1e-4f;
+    if (alpha < -ea || alpha > 1.0f + ea || beta < -eb || beta > 1.0f + eb) return false;
     return true;
 }
 
@@ -502,7 +528,7 @@ __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>
         if (COUNT) cnt[CT_QUAD]++;
         const int code = aquad_code(p);
         if (code != 0) {
-            if (!aquad_maybe(p, code, f.o, f.d, f.a, thi)) return false;
+            if (!aquad_maybe(p, code, f.o, f.d, f.dn, thi)) return false;
             return aquad_t<Real>(p, code, r.o, r.d, K<Real>::TMIN, inf, t);
         }
         if (!planar_maybe<true>(p, f, thi)) return false;

@@ -742,6 +742,13 @@ struct Builder {
             p.g2[0] = v.x; p.g2[1] = v.y; p.g2[2] = v.z;
             p.g3[0] = n.x; p.g3[1] = n.y; p.g3[2] = n.z;
             p.g4[0] = w.x; p.g4[1] = w.y; p.g4[2] = w.z;
+            // general quads: |w||u|, |w||v| (rounded up) scale the kernel's alpha/beta
+            // error margins (pt_kernel.hpp planar_maybe); axis quads re-use the slots
+            {
+                const double wn = std::sqrt(len2<double>(w));
+                p.g1[3] = (float)(wn * std::sqrt(len2<double>(u)) * (1.0 + 1e-5));
+                p.g2[3] = (float)(wn * std::sqrt(len2<double>(v)) * (1.0 + 1e-5));
+            }
             if (p.type == PRIM_QUAD) encode_axis_quad(p, u, v, cp, w);
             if (p.type == PRIM_PLANE) {
                 const double eps = 1e-4;
