@@ -8,7 +8,7 @@ template <bool EMIT, int INSTR, int TRAV, bool LDSS>
 static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                       const SampleBuf* sb, hipStream_t stream) {
     if (sb)
-        hipLaunchKernelGGL((pt_chunk_kernel<float, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+        hipLaunchKernelGGL((pt_chunk_kernel<float, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlockChunk), g.lds_bytes,
                            stream, S, reg, out, g.tiles_x, *sb);
     else
         hipLaunchKernelGGL((pt_render_kernel<float, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,

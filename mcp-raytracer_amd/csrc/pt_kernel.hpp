@@ -92,7 +92,15 @@ constexpr int kBruteMaxPrims = 16;  // AUTO picks BRUTE up to this many primitiv
 #endif
 
 constexpr int kWave = 64;
-constexpr int kBlock = 768;  // 12 waves = 3 per SIMD: one persistent workgroup per CU shares one LDS scene copy
+// Persistent workgroups, one per CU, sharing one LDS scene copy:
+//   sequential kernel 768 threads (12 waves = 3 per SIMD, <= 168 VGPRs),
+//   chunked kernel RT_CHUNK_BLOCK threads (1024: 16 waves = 4 per SIMD, <= 128 VGPRs).
+#ifndef RT_CHUNK_BLOCK
+#define RT_CHUNK_BLOCK 1024
+#endif
+constexpr int kBlock = 768;
+constexpr int kBlockChunk = RT_CHUNK_BLOCK;
+constexpr int kStackStride = 1024;  // LDS traversal-stack column stride (>= any block size)
 constexpr int kTile = 8;          // 8x8 pixels per wave-tile
 constexpr int kEmitStack = 128;   // emission terms kept for the right fold (EMIT builds)
 
@@ -363,7 +371,7 @@ __device__ __forceinline__ bool prim_t(const RtPrim& p, const RayK<Real>& r, Rea
 // BVHNode.hit restated as an explicit DFS with the same visiting order: the
 // box is tested when a node is entered with the closest-so-far interval, left
 // subtree before right, leaf primitives in leaf order with a narrowing max.
-// `stk` points at this lane's column of the LDS stack (stride kBlock ints).
+// `stk` points at this lane's column of the LDS stack (stride kStackStride ints).
 template <class Real, bool COUNT>
 __device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
                                            uint32_t* cnt) {
@@ -387,7 +395,7 @@ __device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& 
                     }
                 }
             } else {
-                stk[sp * kBlock] = nd.b;
+                stk[sp * kStackStride] = nd.b;
                 ++sp;
                 node = nd.a;
                 descend = true;
@@ -396,7 +404,7 @@ __device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& 
         if (!descend) {
             if (sp == 0) break;
             --sp;
-            node = stk[sp * kBlock];
+            node = stk[sp * kStackStride];
         }
     }
     t_hit = tmax;
@@ -587,8 +595,8 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             const bool hb = slab(nd.box[1], f, thi, tb);
             if (ha && hb) {
                 const bool a_first = ta <= tb;
-                stk[sp * kBlock] = a_first ? nd.box[1].a : nd.box[0].a;
-                stkt[sp * kBlock] = a_first ? tb : ta;
+                stk[sp * kStackStride] = a_first ? nd.box[1].a : nd.box[0].a;
+                stkt[sp * kStackStride] = a_first ? tb : ta;
                 ++sp;
                 ref = a_first ? nd.box[0].a : nd.box[1].a;
                 next = true;
@@ -600,8 +608,8 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
         if (!next) {
             while (sp > 0) {
                 --sp;
-                if (stkt[sp * kBlock] <= thi) {
-                    ref = stk[sp * kBlock];
+                if (stkt[sp * kStackStride] <= thi) {
+                    ref = stk[sp * kStackStride];
                     next = true;
                     break;
                 }
@@ -1120,7 +1128,7 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
     DevScene S = S0;
     if (LDSS) {
         uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
-        for (int w = threadIdx.x; w < S0.lds_words; w += kBlock) dst[w] = S0.blob[w];
+        for (int w = threadIdx.x; w < S0.lds_words; w += blockDim.x) dst[w] = S0.blob[w];
         __syncthreads();
         const char* b = reinterpret_cast<const char*>(dst);
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
@@ -1137,7 +1145,7 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
 // INSTR: 0 = product build, 1 = work counters, 2 = section timing.
 // ---------------------------------------------------------------------------
 template <class Real, bool EMIT, int INSTR, int TRAV, bool LDSS>
-__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void pt_render_kernel(DevScene S0, RtRegion reg, RenderOut out,
+__global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion reg, RenderOut out,
                                                                          int tiles_x, int my_tiles) {
     constexpr bool COUNT = INSTR == 1;
     constexpr bool PROF = INSTR == 2;
@@ -1146,7 +1154,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void pt_render_kernel(DevScen
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
     int* stk = lds_stack + threadIdx.x;
-    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C.stack_depth * kBlock + threadIdx.x;
+    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C.stack_depth * kStackStride + threadIdx.x;
 
     const int endX = min(reg.x + reg.width, C.width);
     const int endY = min(reg.y + reg.height, C.height);
@@ -1275,7 +1283,7 @@ __device__ __forceinline__ void item_pixel(const RtRegion& reg, int tiles_x, dou
 }
 
 template <class Real, bool EMIT, int INSTR, int TRAV, bool LDSS>
-__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void pt_chunk_kernel(DevScene S0, RtRegion reg, RenderOut out,
+__global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRegion reg, RenderOut out,
                                                                         int tiles_x, SampleBuf sb) {
     constexpr bool COUNT = INSTR == 1;
     constexpr bool PROF = INSTR == 2;
@@ -1284,7 +1292,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void pt_chunk_kernel(DevScene
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
     int* stk = lds_stack + threadIdx.x;
-    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kBlock + threadIdx.x;
+    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kStackStride + threadIdx.x;
     const int endX = min(reg.x + reg.width, C0.width);
     const int endY = min(reg.y + reg.height, C0.height);
     const int n_items = sb.n_items;

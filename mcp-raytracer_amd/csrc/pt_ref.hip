@@ -9,7 +9,7 @@ template <bool EMIT, int INSTR, int TRAV, bool LDSS>
 static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                       const SampleBuf* sb, hipStream_t stream) {
     if (sb)
-        hipLaunchKernelGGL((pt_chunk_kernel<double, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+        hipLaunchKernelGGL((pt_chunk_kernel<double, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlockChunk), g.lds_bytes,
                            stream, S, reg, out, g.tiles_x, *sb);
     else
         hipLaunchKernelGGL((pt_render_kernel<double, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
     const RayK<double> r = make_ray<double>(o, d);
     double t = 0;
     int* stk = lds_stack + threadIdx.x;
-    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)S.cam.stack_depth * kBlock + threadIdx.x;
+    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)S.cam.stack_depth * kStackStride + threadIdx.x;
     const int h = closest_hit_any<double, false, TRAV>(S, S.cam.n_prims, r, t, stk, stkt, nullptr);
     double* w = out + 10 * (size_t)k;
     w[0] = h >= 0;

@@ -207,8 +207,8 @@ struct rt_camera {
         // Fixed spp: the chunked kernel balances small images (few tiles per
         // resident wave) far better; large images already balance over tiles and
         // skip the sample-buffer round trip.
-        const long resident_waves = (long)cus * (kBlock / kWave);
-        const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 8 * resident_waves);
+        const long resident_waves = (long)cus * (kBlockChunk / kWave);
+        const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 4 * resident_waves);
         if (C.adaptive || C.n_samples <= 0 || !chunked) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
             hip_check(hipEventRecord(ev[0], stream), "hipEventRecord");
@@ -273,7 +273,7 @@ struct rt_camera {
             sb.n_items = (int32_t)items;
             if (t0 > 0) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = g;
-            gp.grid = (int)std::max<long>(1, std::min<long>(items / kBlock + 1, (long)cus));
+            gp.grid = (int)std::max<long>(1, std::min<long>(items / kBlockChunk + 1, (long)cus));
             if (t0 == 0) hip_check(hipEventRecord(ev[0], stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, gp, &sb, stream)
                                              : launch_render_ref(v, S, reg, out, gp, &sb, stream);
