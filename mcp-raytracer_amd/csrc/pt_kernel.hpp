@@ -98,7 +98,10 @@ constexpr int kWave = 64;
 #ifndef RT_CHUNK_BLOCK
 #define RT_CHUNK_BLOCK 1024
 #endif
-constexpr int kBlock = 768;
+#ifndef RT_SEQ_BLOCK
+#define RT_SEQ_BLOCK 768
+#endif
+constexpr int kBlock = RT_SEQ_BLOCK;
 constexpr int kBlockChunk = RT_CHUNK_BLOCK;
 constexpr int kStackStride = 1024;  // LDS traversal-stack column stride (>= any block size)
 constexpr int kTile = 8;          // 8x8 pixels per wave-tile
@@ -108,14 +111,9 @@ constexpr int kEmitStack = 128;   // emission terms kept for the right fold (EMI
 // Seeded replacement for Math.random: PCG32 (XSH-RR) stream per (seed, pixel,
 // sample), consumed in the reference's draw order.
 // ---------------------------------------------------------------------------
-__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-__device__ __forceinline__ uint64_t rng_init(uint32_t seed, uint32_t pixel, uint32_t sample) {
-    return splitmix64((((uint64_t)pixel << 32) | sample) ^ splitmix64(seed));
+// seed_mix = splitmix64(seed), precomputed per camera (RtCamera::seed_mix)
+__device__ __forceinline__ uint64_t rng_init(uint64_t seed_mix, uint32_t pixel, uint32_t sample) {
+    return splitmix64((((uint64_t)pixel << 32) | sample) ^ seed_mix);
 }
 __device__ __forceinline__ uint32_t rng_u32(uint64_t& s) {
     const uint64_t old = s;
@@ -895,12 +893,16 @@ struct Path {
 };
 
 // Camera.getRay (src/camera.ts:176-210) for sample `sample` of pixel (i, j).
+// pixel00Loc + i*pixelDeltaU + j*pixelDeltaV (src/camera.ts:181), fixed per pixel.
+template <class Real>
+__device__ __forceinline__ V3 pixel_center(const RtCamera& C, int i, int j) {
+    return add(add(ld3(C.pixel00), scale<Real>(ld3(C.du), (Real)i)), scale<Real>(ld3(C.dv), (Real)j));
+}
+
 template <class Real, bool EMIT>
-__device__ __forceinline__ void path_begin(const RtCamera& C, Path<EMIT>& P, int i, int j, uint32_t pix,
-                                           uint32_t sample) {
-    P.rng = rng_init(C.seed, pix, sample);
-    const V3 p00 = ld3(C.pixel00), du = ld3(C.du), dv = ld3(C.dv), cen = ld3(C.center);
-    const V3 pc = add(add(p00, scale<Real>(du, (Real)i)), scale<Real>(dv, (Real)j));
+__device__ __forceinline__ void path_begin(const RtCamera& C, Path<EMIT>& P, V3 pc, uint32_t pix, uint32_t sample) {
+    P.rng = rng_init(C.seed_mix, pix, sample);
+    const V3 du = ld3(C.du), dv = ld3(C.dv), cen = ld3(C.center);
     V3 ps = pc;
     if (C.samples > 1.0) {
         const Real px = (Real)-0.5 + uniform<Real>(P.rng);
@@ -1199,7 +1201,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
             const RtCamera& C = cam_opaque();
             if (PROF) { pf.tl = pf.tt; pf.secs[PR_TRIPS]++; }
             if (new_path) {
-                path_begin<Real, EMIT>(C, P, i, j, pix, (uint32_t)n);
+                path_begin<Real, EMIT>(C, P, pixel_center<Real>(C, i, j), pix, (uint32_t)n);
                 new_path = false;
                 psec<PROF>(pf, PR_NEWPATH);
             }
@@ -1315,6 +1317,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     int slot = -1;                    // this lane's pixel slot (-1: idle)
     int s = 0, s_end = 0, i = 0, j = 0;
     uint32_t pix = 0;
+    V3 pc = v3(0, 0, 0);  // the current item's pixel centre
     bool new_path = false;
     Path<EMIT> P;
     const double rtx = 1.0 / (double)tiles_x;
@@ -1354,6 +1357,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                         s = sb.s0[ph] + ch * sb.chunk[ph];
                         s_end = s + sb.chunk[ph];
                         pix = (uint32_t)j * (uint32_t)C0.width + (uint32_t)i;
+                        pc = pixel_center<Real>(cam_opaque(), i, j);
                         new_path = true;
                     }
                 }
@@ -1368,7 +1372,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             const RtCamera& C = cam_opaque();
             if (PROF) { pf.tl = pf.tt; pf.secs[PR_TRIPS]++; }
             if (new_path) {
-                path_begin<Real, EMIT>(C, P, i, j, pix, (uint32_t)s);
+                path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)s);
                 new_path = false;
             }
             psec<PROF>(pf, PR_NEWPATH);

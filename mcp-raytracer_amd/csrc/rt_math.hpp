@@ -114,6 +114,14 @@ RT_HD Real js_max(Real a, Real b) {
 template <class Real>
 RT_HD V3 ray_at(V3 o, V3 d, Real t) { return add(o, scale<Real>(d, t)); }
 
+// splitmix64 finaliser (seeds the per-path PCG32 streams, pt_kernel.hpp rng_init).
+RT_HD uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 // Color.illuminance (src/geometry/vec3.ts:239-242), always a JS double.
 RT_HD double illuminance(V3 c) { return 0.299 * (double)c.x + 0.587 * (double)c.y + 0.114 * (double)c.z; }
 

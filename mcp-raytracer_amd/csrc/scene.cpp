@@ -1115,6 +1115,7 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
     cam.n_prims = (int32_t)b.out.prims.size();
     cam.n_mats = (int32_t)b.out.mats.size();
     cam.seed = (uint32_t)(int64_t)seed;
+    cam.seed_mix = splitmix64(cam.seed);
     cam.stack_depth = b.out.bvh_depth + 1;
     b.out.fnodes = make_fast_nodes(b.out.nodes);
     b.out.tnodes = make_tnodes(b.out.fnodes, b.out.troot);

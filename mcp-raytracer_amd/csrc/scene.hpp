@@ -114,6 +114,7 @@ struct RtCamera {
     int32_t n_prims;
     int32_t n_mats;
     uint32_t seed;
+    uint64_t seed_mix;    // splitmix64(seed): per-path RNG keys derive from it
     int32_t stack_depth;  // BVH traversal stack entries needed (tree depth + 1)
 };
 
