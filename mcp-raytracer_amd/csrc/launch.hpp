@@ -47,7 +47,7 @@ hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float*
 inline size_t stack_lds_bytes(int stack_depth, int trav) {
     if (trav == TRAV_BRUTE) return 0;
     const size_t d = (size_t)(stack_depth > 0 ? stack_depth : 1);
-    return d * kStackStride * (trav == TRAV_FAST ? 2 * sizeof(int) : sizeof(int));
+    return d * kStackStride * ((trav == TRAV_FAST && kStackTnear) ? 2 * sizeof(int) : sizeof(int));
 }
 
 }  // namespace rt

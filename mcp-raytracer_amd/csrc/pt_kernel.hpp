@@ -32,19 +32,21 @@
 
 namespace rt {
 
-// The scene lives in one device buffer ("blob"): [tnodes][prims][mats][lights][nodes],
+// The scene lives in one device buffer ("blob"): [tnodes][tprims][prims][mats][lights][nodes],
 // 16-byte aligned sections. When [tnodes][prims] fits, every workgroup copies
 // it into LDS (LDS-resident launch): traversal and primitive reads are LDS reads.
 struct DevScene {
     const RtTNode* __restrict__ tnodes; // fast traversal: children-in-parent nodes (blob start)
     const RtPrim* __restrict__ prims;   // global, or LDS in an LDS-resident launch
     const RtPrim* __restrict__ gprims;  // always the global copy (scalar-load reads)
+    const int32_t* __restrict__ tprims; // fast-traversal leaves -> primitive slots (LDS when resident)
     const RtMat* __restrict__ mats;
     const RtLight* __restrict__ lights;
     const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
-    const uint4* __restrict__ blob;     // the whole scene: [tnodes][prims][mats][lights][nodes]
-    int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS ([tnodes][prims])
+    const uint4* __restrict__ blob;     // the whole scene: [tnodes][tprims][prims][mats][lights][nodes]
+    int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS ([tnodes][tprims][prims])
     int32_t off_prims;                  // byte offset of prims in the blob
+    int32_t off_tprims;                 // byte offset of tprims in the blob
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
@@ -104,6 +106,13 @@ constexpr int kWave = 64;
 constexpr int kBlock = RT_SEQ_BLOCK;
 constexpr int kBlockChunk = RT_CHUNK_BLOCK;
 constexpr int kStackStride = 1024;  // LDS traversal-stack column stride (>= any block size)
+// Fast traversal stack entries: node reference only (4 B; a popped subtree is
+// culled one level later by its children's slab tests), or also its entry
+// distance (8 B; culled on pop). 4 B keeps deeper SAH trees LDS-resident.
+#ifndef RT_STACK_TNEAR
+#define RT_STACK_TNEAR 0
+#endif
+constexpr bool kStackTnear = RT_STACK_TNEAR != 0;
 constexpr int kTile = 8;          // 8x8 pixels per wave-tile
 constexpr int kEmitStack = 128;   // emission terms kept for the right fold (EMIT builds)
 
@@ -577,7 +586,8 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             const int v = ~ref;
             const int first = v >> 3;
             const int end = first + (v & 7);
-            for (int k = first; k < end; ++k) {
+            for (int m = first; m < end; ++m) {
+                const int k = S.tprims[m];  // reference leaf slot (the tie-break key)
                 Real t;
                 if (prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt) && (t < best_t || (t == best_t && k < best))) {
                     best_t = t;
@@ -594,7 +604,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             if (ha && hb) {
                 const bool a_first = ta <= tb;
                 stk[sp * kStackStride] = a_first ? nd.box[1].a : nd.box[0].a;
-                stkt[sp * kStackStride] = a_first ? tb : ta;
+                if (kStackTnear) stkt[sp * kStackStride] = a_first ? tb : ta;
                 ++sp;
                 ref = a_first ? nd.box[0].a : nd.box[1].a;
                 next = true;
@@ -606,7 +616,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
         if (!next) {
             while (sp > 0) {
                 --sp;
-                if (stkt[sp * kStackStride] <= thi) {
+                if (!kStackTnear || stkt[sp * kStackStride] <= thi) {
                     ref = stk[sp * kStackStride];
                     next = true;
                     break;
@@ -1134,6 +1144,7 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
         __syncthreads();
         const char* b = reinterpret_cast<const char*>(dst);
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
+        S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
         S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
     }
     return S;

@@ -70,7 +70,7 @@ struct rt_camera {
     int device = -1;
     uint4* d_blob = nullptr;  // [tnodes][prims][mats][lights][nodes] (DevScene)
     int32_t lds_words = 0;    // [tnodes][prims] prefix, 16-byte words
-    int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0;
+    int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // path start, path end, accumulate end
     bool ev_recorded = false, ev_accum = false;
@@ -102,7 +102,7 @@ struct rt_camera {
 
     template <class T>
     static void append(std::vector<char>& blob, const std::vector<T>& v, int32_t* off) {
-        static_assert(sizeof(T) % 16 == 0, "scene records are 16-byte multiples");
+        if ((v.size() * sizeof(T)) % 16) throw std::runtime_error("blob sections must be 16-byte multiples");
         if (off) *off = (int32_t)blob.size();
         const char* p = reinterpret_cast<const char*>(v.data());
         blob.insert(blob.end(), p, p + v.size() * sizeof(T));
@@ -115,6 +115,7 @@ struct rt_camera {
         if (device >= 0) release();
         std::vector<char> blob;
         append(blob, build.tnodes, nullptr);
+        append(blob, build.tprims, &off_tprims);
         append(blob, build.prims, &off_prims);
         lds_words = (int32_t)(blob.size() / 16);
         append(blob, build.mats, &off_mats);
@@ -154,6 +155,8 @@ struct rt_camera {
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.prims = reinterpret_cast<const RtPrim*>(b + off_prims);
         S.gprims = S.prims;
+        S.tprims = reinterpret_cast<const int32_t*>(b + off_tprims);
+        S.off_tprims = off_tprims;
         S.mats = reinterpret_cast<const RtMat*>(b + off_mats);
         S.lights = reinterpret_cast<const RtLight*>(b + off_lights);
         S.nodes = reinterpret_cast<const RtNode*>(b + off_nodes);
@@ -162,7 +165,7 @@ struct rt_camera {
         S.off_prims = off_prims;
         S.lds_stack_bytes = 0;
         S.troot = build.troot;
-        S.root_box = build.fnodes.empty() ? RtNode{} : build.fnodes[0];
+        S.root_box = build.troot_box;
         S.cam = build.cam;
         S.mix_total = mix_total;
         S.light_w = light_w;

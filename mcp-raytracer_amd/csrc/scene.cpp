@@ -929,6 +929,120 @@ std::vector<RtTNode> make_tnodes(const std::vector<RtNode>& f, int32_t& root_ref
     return out;
 }
 
+// ---------------------------------------------------------------------------
+// Fast-traversal tree built for speed, not for the reference's visiting order:
+// the fast traversal returns the (t, slot) minimum over all primitives, so any
+// tree whose boxes enclose their primitives gives the reference's hit. Binned
+// SAH (16 bins on the longest centroid axis, leaves of <= 4), falling back to
+// median splits where the depth would outgrow the LDS traversal stack. Leaves
+// index `order` (-> SceneBuild::tprims), i.e. reference leaf slots.
+// ---------------------------------------------------------------------------
+struct SahBuilder {
+    const std::vector<Box>& pbox;  // per slot
+    std::vector<int32_t> order;
+    std::vector<RtNode> nodes;     // DFS, RtNode conventions (leaf: a = first, b = -count)
+    int cap;                       // maximum depth (root = 1)
+    int depth_seen = 0;
+
+    SahBuilder(const std::vector<Box>& b, int cap_) : pbox(b), cap(cap_) {
+        order.resize(b.size());
+        for (size_t i = 0; i < b.size(); ++i) order[i] = (int32_t)i;
+    }
+    static double area(const Box& b) {
+        const double dx = (double)b.mx.x - b.mn.x, dy = (double)b.mx.y - b.mn.y, dz = (double)b.mx.z - b.mn.z;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+    static Box merge(const Box& a, const Box& b) {
+        return Box{v3(std::min(a.mn.x, b.mn.x), std::min(a.mn.y, b.mn.y), std::min(a.mn.z, b.mn.z)),
+                   v3(std::max(a.mx.x, b.mx.x), std::max(a.mx.y, b.mx.y), std::max(a.mx.z, b.mx.z))};
+    }
+    static float cen(const Box& b, int a) { return 0.5f * (comp(b.mn, a) + comp(b.mx, a)); }
+
+    int build(int begin, int end, int depth) {
+        depth_seen = std::max(depth_seen, depth);
+        const int idx = (int)nodes.size();
+        nodes.push_back(RtNode{});
+        Box bb = pbox[(size_t)order[(size_t)begin]];
+        Box cb{v3(INFINITY, INFINITY, INFINITY), v3(-INFINITY, -INFINITY, -INFINITY)};
+        for (int i = begin; i < end; ++i) {
+            const Box& b = pbox[(size_t)order[(size_t)i]];
+            bb = merge(bb, b);
+            const V3 c = v3(cen(b, 0), cen(b, 1), cen(b, 2));
+            cb = merge(cb, Box{c, c});
+        }
+        auto set_box = [&](RtNode& n) {
+            n.bmin[0] = bb.mn.x; n.bmin[1] = bb.mn.y; n.bmin[2] = bb.mn.z;
+            n.bmax[0] = bb.mx.x; n.bmax[1] = bb.mx.y; n.bmax[2] = bb.mx.z;
+        };
+        const int count = end - begin;
+        auto make_leaf = [&]() {
+            RtNode& n = nodes[(size_t)idx];
+            set_box(n);
+            n.a = begin;
+            n.b = -count;
+            return idx;
+        };
+        if (count <= 2) return make_leaf();
+        int axis = 0;
+        float ext[3] = {cb.mx.x - cb.mn.x, cb.mx.y - cb.mn.y, cb.mx.z - cb.mn.z};
+        if (ext[1] > ext[axis]) axis = 1;
+        if (ext[2] > ext[axis]) axis = 2;
+        int mid = -1;
+        const int need = (int)std::ceil(std::log2(std::max(1.0, count / 4.0)));
+        if (ext[axis] > 0.0f && depth + need + 2 < cap) {
+            constexpr int kBins = 16;
+            Box binb[kBins];
+            int binn[kBins] = {0};
+            const float lo = comp(cb.mn, axis), scale = kBins / ext[axis];
+            auto bin_of = [&](const Box& b) {
+                int k = (int)((cen(b, axis) - lo) * scale);
+                return std::min(std::max(k, 0), kBins - 1);
+            };
+            for (int i = begin; i < end; ++i) {
+                const Box& b = pbox[(size_t)order[(size_t)i]];
+                const int k = bin_of(b);
+                binb[k] = binn[k] ? merge(binb[k], b) : b;
+                ++binn[k];
+            }
+            double best = INFINITY;
+            int best_k = -1;
+            for (int k = 1; k < kBins; ++k) {  // split between bin k-1 and k
+                Box lb{}, rb{};
+                int ln = 0, rn = 0;
+                for (int q = 0; q < k; ++q) if (binn[q]) { lb = ln ? merge(lb, binb[q]) : binb[q]; ln += binn[q]; }
+                for (int q = k; q < kBins; ++q) if (binn[q]) { rb = rn ? merge(rb, binb[q]) : binb[q]; rn += binn[q]; }
+                if (!ln || !rn) continue;
+                const double c = area(lb) * ln + area(rb) * rn;
+                if (c < best) { best = c; best_k = k; }
+            }
+            const double leaf_cost = (double)count;
+            const double split_cost = 1.0 + best / std::max(area(bb), 1e-30);
+            if (count <= 4 && !(split_cost < leaf_cost)) return make_leaf();
+            if (best_k > 0) {
+                auto it = std::partition(order.begin() + begin, order.begin() + end,
+                                         [&](int32_t s) { return bin_of(pbox[(size_t)s]) < best_k; });
+                mid = (int)(it - order.begin());
+                if (mid == begin || mid == end) mid = -1;
+            }
+        }
+        if (mid < 0) {  // median split by centroid (balanced; also for coincident centroids)
+            if (count <= 4) return make_leaf();
+            mid = begin + count / 2;
+            std::nth_element(order.begin() + begin, order.begin() + mid, order.begin() + end, [&](int32_t x, int32_t y) {
+                const float cx = cen(pbox[(size_t)x], axis), cy = cen(pbox[(size_t)y], axis);
+                return cx < cy || (cx == cy && x < y);
+            });
+        }
+        const int l = build(begin, mid, depth + 1);
+        const int r = build(mid, end, depth + 1);
+        RtNode& n = nodes[(size_t)idx];
+        set_box(n);
+        n.a = l;
+        n.b = r;
+        return idx;
+    }
+};
+
 // The fast traversal is exact only if no primitive can be hit outside the box
 // the reference gives it: a negative-radius sphere (inverted box, e.g. the
 // default scene's hollow glass), a NaN bound, or a plane whose normal passes
@@ -1116,9 +1230,39 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
     cam.n_mats = (int32_t)b.out.mats.size();
     cam.seed = (uint32_t)(int64_t)seed;
     cam.seed_mix = splitmix64(cam.seed);
-    cam.stack_depth = b.out.bvh_depth + 1;
     b.out.fnodes = make_fast_nodes(b.out.nodes);
-    b.out.tnodes = make_tnodes(b.out.fnodes, b.out.troot);
+    // fast-traversal tree: SAH over the reference's per-object boxes (finite boxes
+    // only, i.e. no planes), else the reference tree itself
+    {
+        std::vector<Box> slot_box(b.out.prims.size());
+        bool finite = true;
+        for (size_t k = 0; k < slot_box.size(); ++k) {
+            slot_box[k] = b.boxes[(size_t)b.out.prim_object[k]];
+            const Box& x = slot_box[k];
+            for (float v : {x.mn.x, x.mn.y, x.mn.z, x.mx.x, x.mx.y, x.mx.z})
+                if (!std::isfinite(v)) finite = false;
+            if (!(x.mn.x <= x.mx.x && x.mn.y <= x.mx.y && x.mn.z <= x.mx.z)) finite = false;
+        }
+        const char* env = std::getenv("RT_AMD_SAH");
+        const bool sah = finite && slot_box.size() > 16 && !(env && env[0] == '0');
+        if (sah) {
+            SahBuilder sb(slot_box, std::max(b.out.bvh_depth + 2, 12));
+            sb.build(0, (int)slot_box.size(), 1);
+            b.out.tprims = sb.order;
+            const std::vector<RtNode> padded = make_fast_nodes(sb.nodes);
+            b.out.tnodes = make_tnodes(padded, b.out.troot);
+            b.out.troot_box = padded[0];
+            b.out.tdepth = sb.depth_seen;
+        } else {
+            b.out.tprims.resize(b.out.prims.size());
+            for (size_t k = 0; k < b.out.tprims.size(); ++k) b.out.tprims[k] = (int32_t)k;
+            b.out.tnodes = make_tnodes(b.out.fnodes, b.out.troot);
+            b.out.troot_box = b.out.fnodes[0];
+            b.out.tdepth = b.out.bvh_depth;
+        }
+        b.out.tprims.resize((b.out.tprims.size() + 3) / 4 * 4, 0);  // 16-byte blob sections
+    }
+    cam.stack_depth = std::max(b.out.bvh_depth, b.out.tdepth) + 1;
     b.out.fast_ok = prims_inside_boxes(b.out.prims);
     return std::move(b.out);
 }

@@ -130,8 +130,11 @@ struct RtRegion {
 struct SceneBuild {
     std::vector<RtNode> nodes;
     std::vector<RtNode> fnodes;  // same tree, boxes for the fast traversal (padded / reject-marked)
-    std::vector<RtTNode> tnodes; // fnodes re-laid out children-in-parent (fast traversal)
+    std::vector<RtTNode> tnodes; // fast-traversal tree, children-in-parent (SAH, or the reference tree)
+    std::vector<int32_t> tprims; // its leaves' primitive slots (padded to a multiple of 4)
     int32_t troot = 0;           // reference of the root (TNode index or leaf code)
+    int tdepth = 0;              // its depth (root = 1)
+    RtNode troot_box{};          // its root box (padded)
     std::vector<RtPrim> prims;
     std::vector<RtMat> mats;
     std::vector<RtLight> lights;
