@@ -27,6 +27,8 @@ SCENES = {
     "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}}, {"aspect": 1}),
     "rain": ({"type": "rain", "options": {"seed": 42}}, {}),
     "default": ({"type": "default"}, {}),
+    # BASELINE config 5: 100k requested, ~76.6k placed by the reference's rule
+    "spheres100k": ({"type": "spheres", "options": {"count": 100000, "seed": 42}}, {"aspect": 1}),
 }
 
 

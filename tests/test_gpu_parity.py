@@ -257,3 +257,78 @@ def test_generate_image_buffer_png(rt, gpu):
     png2 = rt.generate_image_buffer({"type": "cornell", "render": {"width": 24, "samples": 4, "depth": 4}},
                                     {"parallel": True, "threads": 5})
     assert png2 == png  # the band split never changes pixels (RNG keyed by pixel/sample)
+
+
+def _hit_equal(rt, oracle, sd, o, d, travs=("reference", "fast", "brute")):
+    """world_hit under every strategy vs the oracle: hit flag, t, p, n, front, object."""
+    cam = rt.create_camera_from_scene_data(sd, {"width": 8})
+    c = oracle.world_hit(sd, o, d)
+    po = cam.export()["prim_object"]
+    for trav in travs:
+        g = cam.debug_world_hit(o, d, traversal=trav)
+        assert np.array_equal(g[:, 0], c[:, 0]), trav
+        h = g[:, 0] > 0
+        assert np.array_equal(g[h, 1], c[h, 1]), trav
+        assert np.array_equal(g[h, 2:9], c[h, 2:9]), trav
+        assert np.array_equal(po[g[h, 9].astype(int)], c[h, 9].astype(int)), trav
+    return c
+
+
+def test_axis_quad_edges_and_corners(rt, oracle, gpu):
+    """Cornell walls are axis-aligned quads (aquad_t): rays aimed exactly at
+    edges, corners and just outside them must decide alpha/beta like the
+    reference's general formula."""
+    sd = rt.generate_scene_data({"type": "cornell"})
+    rng = np.random.default_rng(11)
+    targets = []
+    for obj in sd["objects"]:
+        if obj["type"] != "quad":
+            continue
+        q, u, v = (np.array(obj[k], np.float64) for k in ("pos", "u", "v"))
+        for a in (0.0, 1.0, 0.5, 1e-7, 1 - 1e-7, -1e-7, 1 + 1e-7):
+            for b in (0.0, 1.0, 0.25, -1e-7, 1 + 1e-7):
+                targets.append(q + a * u + b * v)
+    targets = np.array(targets)
+    n = len(targets)
+    o = rng.uniform(50, 500, (n, 3))
+    d = (targets - o).astype(np.float32)
+    c = _hit_equal(rt, oracle, sd, o.astype(np.float32), d)
+    assert (c[:, 0] > 0).mean() > 0.5
+
+
+def test_sah_tree_on_surface_and_grazing_rays(rt, oracle, gpu):
+    """spheres-500 (SAH fast tree): secondary-ray-like origins on sphere surfaces,
+    tangent directions, and far/axis-parallel rays."""
+    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 500, "seed": 42}})
+    rng = np.random.default_rng(5)
+    sph = [ob for ob in sd["objects"] if ob["type"] == "sphere"]
+    n = 6000
+    idx = rng.integers(0, len(sph), n)
+    c = np.array([sph[k]["pos"] for k in idx], np.float64)
+    r = np.array([sph[k]["r"] for k in idx], np.float64)
+    nrm = rng.normal(size=(n, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    o = (c + np.abs(r)[:, None] * nrm).astype(np.float32)   # on the surface
+    d = rng.normal(size=(n, 3))
+    d[: n // 3] -= (d[: n // 3] * nrm[: n // 3]).sum(1, keepdims=True) * nrm[: n // 3]  # tangent
+    d[n // 3: n // 2, rng.integers(0, 3)] = 0.0
+    far = rng.uniform(-50, 50, (n // 4, 3)).astype(np.float32)
+    o[-(n // 4):] = far
+    _hit_equal(rt, oracle, sd, o, d.astype(np.float32), travs=("reference", "fast"))
+
+
+@pytest.mark.parametrize("name", ["cornell", "spheres", "rain"])
+def test_chunked_kernel_equals_sequential(rt, gpu, name, monkeypatch):
+    """The chunked kernel (lane work pool + in-order accumulate) reproduces the
+    sequential kernel's image and stats bit for bit."""
+    cfg, ro = _cfgs()[name]
+    sd = rt.generate_scene_data(cfg)
+    ro = {**ro, "width": 160, "samples": 37}  # odd spp: every guided phase, partial tiles
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RT_AMD_CHUNKED", flag)
+        cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+        outs.append((rgb, rad, st))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1], equal_nan=True)
+    assert outs[0][2].samples == outs[1][2].samples and outs[0][2].bounces == outs[1][2].bounces
