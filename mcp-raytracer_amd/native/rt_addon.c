@@ -1,0 +1,211 @@
+/* N-API addon: the binding df07/mcp-raytracer's TypeScript host loads instead of
+ * building its object-model Camera.
+ *
+ * Replaces, one-for-one:
+ *   createCameraFromSceneData(sceneData, renderOptions)  src/scenes/scenes.ts:60-104
+ *   camera.renderRegion(buffer, region) -> RenderStats  src/camera.ts:388-431
+ *   generateSceneData(sceneConfig)                      src/scenes/scenes.ts:42-50
+ * through include/rt_amd.h. Errors are thrown as JS Errors carrying the same
+ * messages the reference throws (rt_last_error()).
+ *
+ * Built in-tree against Node's node_api.h (raytracer_amd/_build.py build_addon),
+ * linked to librt_amd.so next to it (rpath $ORIGIN). */
+#include <node_api.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rt_amd.h"
+
+#define CHECK_NAPI(env, call)                                      \
+    do {                                                           \
+        if ((call) != napi_ok) {                                   \
+            napi_throw_error((env), NULL, "N-API call failed: " #call); \
+            return NULL;                                           \
+        }                                                          \
+    } while (0)
+
+static napi_value throw_rt(napi_env env) {
+    napi_throw_error(env, NULL, rt_last_error());
+    return NULL;
+}
+
+/* UTF-8 copy of a JS string argument (caller frees); NULL for undefined/null. */
+static char* get_string(napi_env env, napi_value v) {
+    napi_valuetype t;
+    if (napi_typeof(env, v, &t) != napi_ok || t == napi_undefined || t == napi_null) return NULL;
+    size_t n = 0;
+    if (napi_get_value_string_utf8(env, v, NULL, 0, &n) != napi_ok) return NULL;
+    char* s = (char*)malloc(n + 1);
+    if (!s) return NULL;
+    napi_get_value_string_utf8(env, v, s, n + 1, &n);
+    return s;
+}
+
+static void finalize_camera(napi_env env, void* data, void* hint) {
+    (void)env;
+    (void)hint;
+    rt_camera_destroy((rt_camera*)data);
+}
+
+/* generateSceneData(type: string, optionsJson?: string) -> string (SceneData JSON) */
+static napi_value GenerateSceneData(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    char* type = argc > 0 ? get_string(env, argv[0]) : NULL;
+    char* opts = argc > 1 ? get_string(env, argv[1]) : NULL;
+    char* out = NULL;
+    const int rc = rt_generate_scene_data(type ? type : "default", opts, &out);
+    free(type);
+    free(opts);
+    if (rc) return throw_rt(env);
+    napi_value s;
+    const napi_status st = napi_create_string_utf8(env, out, NAPI_AUTO_LENGTH, &s);
+    rt_free(out);
+    if (st != napi_ok) return NULL;
+    return s;
+}
+
+/* createCamera(sceneDataJson: string, renderOptionsJson?: string) -> External<rt_camera> */
+static napi_value CreateCamera(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    char* scene = argc > 0 ? get_string(env, argv[0]) : NULL;
+    char* opts = argc > 1 ? get_string(env, argv[1]) : NULL;
+    rt_camera* cam = NULL;
+    const int rc = rt_camera_create(scene ? scene : "", opts, &cam);
+    free(scene);
+    free(opts);
+    if (rc) return throw_rt(env);
+    napi_value ext;
+    CHECK_NAPI(env, napi_create_external(env, cam, finalize_camera, NULL, &ext));
+    return ext;
+}
+
+static rt_camera* get_camera(napi_env env, napi_value v) {
+    void* p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+        napi_throw_type_error(env, NULL, "expected a camera created by createCamera");
+        return NULL;
+    }
+    return (rt_camera*)p;
+}
+
+static void put_number(napi_env env, napi_value obj, const char* key, double v) {
+    napi_value n;
+    napi_create_double(env, v, &n);
+    napi_set_named_property(env, obj, key, n);
+}
+
+/* cameraInfo(cam) -> { imageWidth, imageHeight, channels, objects, lights, traversal, precision } */
+static napi_value CameraInfo(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rt_camera* cam = argc > 0 ? get_camera(env, argv[0]) : NULL;
+    if (!cam) return NULL;
+    rt_camera_info ci;
+    if (rt_camera_get_info(cam, &ci)) return throw_rt(env);
+    napi_value o;
+    CHECK_NAPI(env, napi_create_object(env, &o));
+    put_number(env, o, "imageWidth", ci.width);
+    put_number(env, o, "imageHeight", ci.height);
+    put_number(env, o, "channels", ci.channels);
+    put_number(env, o, "objects", ci.n_objects);
+    put_number(env, o, "lights", ci.n_lights);
+    put_number(env, o, "traversal", ci.traversal);
+    put_number(env, o, "precision", ci.precision);
+    return o;
+}
+
+static int get_int_prop(napi_env env, napi_value obj, const char* key, int32_t* out) {
+    napi_value v;
+    if (napi_get_named_property(env, obj, key, &v) != napi_ok) return 0;
+    double d = 0;
+    if (napi_get_value_double(env, v, &d) != napi_ok) return 0;
+    *out = (int32_t)d;
+    return 1;
+}
+
+/* renderRegion(cam, buffer: Uint8ClampedArray | Uint8Array (width*height*3, may be
+ * SharedArrayBuffer-backed), region: {x, y, width, height}) -> RenderStats
+ * (src/render-utils/renderStats.ts:6-19 shape). Only the region is written. */
+static napi_value RenderRegion(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 3) {
+        napi_throw_type_error(env, NULL, "renderRegion(camera, buffer, region)");
+        return NULL;
+    }
+    rt_camera* cam = get_camera(env, argv[0]);
+    if (!cam) return NULL;
+    bool is_ta = false;
+    CHECK_NAPI(env, napi_is_typedarray(env, argv[1], &is_ta));
+    if (!is_ta) {
+        napi_throw_type_error(env, NULL, "buffer must be a Uint8ClampedArray");
+        return NULL;
+    }
+    napi_typedarray_type tt;
+    size_t len = 0, off = 0;
+    void* data = NULL;
+    napi_value ab;
+    CHECK_NAPI(env, napi_get_typedarray_info(env, argv[1], &tt, &len, &data, &ab, &off));
+    if (tt != napi_uint8_clamped_array && tt != napi_uint8_array) {
+        napi_throw_type_error(env, NULL, "buffer must be a Uint8ClampedArray");
+        return NULL;
+    }
+    rt_camera_info ci;
+    if (rt_camera_get_info(cam, &ci)) return throw_rt(env);
+    if (len < (size_t)ci.width * (size_t)ci.height * 3u) {
+        napi_throw_range_error(env, NULL, "buffer is smaller than width*height*3");
+        return NULL;
+    }
+    rt_region r;
+    if (!get_int_prop(env, argv[2], "x", &r.x) || !get_int_prop(env, argv[2], "y", &r.y) ||
+        !get_int_prop(env, argv[2], "width", &r.width) || !get_int_prop(env, argv[2], "height", &r.height)) {
+        napi_throw_type_error(env, NULL, "region must be {x, y, width, height}");
+        return NULL;
+    }
+    rt_render_stats s;
+    if (rt_camera_render_region(cam, &r, (uint8_t*)data, NULL, &s)) return throw_rt(env);
+    napi_value out, sm, bo;
+    CHECK_NAPI(env, napi_create_object(env, &out));
+    CHECK_NAPI(env, napi_create_object(env, &sm));
+    CHECK_NAPI(env, napi_create_object(env, &bo));
+    put_number(env, out, "pixels", s.pixels);
+    put_number(env, sm, "total", s.samples_total);
+    put_number(env, sm, "min", s.samples_min);
+    put_number(env, sm, "max", s.samples_max);
+    put_number(env, sm, "avg", s.samples_avg);
+    put_number(env, bo, "total", s.bounces_total);
+    put_number(env, bo, "min", s.bounces_min);
+    put_number(env, bo, "max", s.bounces_max);
+    put_number(env, bo, "avg", s.bounces_avg);
+    napi_set_named_property(env, out, "samples", sm);
+    napi_set_named_property(env, out, "bounces", bo);
+    return out;
+}
+
+static napi_value Version(napi_env env, napi_callback_info info) {
+    (void)info;
+    napi_value v;
+    napi_create_int32(env, rt_version(), &v);
+    return v;
+}
+
+static napi_value Init(napi_env env, napi_value exports) {
+    napi_property_descriptor d[] = {
+        {"generateSceneData", NULL, GenerateSceneData, NULL, NULL, NULL, napi_default, NULL},
+        {"createCamera", NULL, CreateCamera, NULL, NULL, NULL, napi_default, NULL},
+        {"cameraInfo", NULL, CameraInfo, NULL, NULL, NULL, napi_default, NULL},
+        {"renderRegion", NULL, RenderRegion, NULL, NULL, NULL, napi_default, NULL},
+        {"version", NULL, Version, NULL, NULL, NULL, napi_default, NULL},
+    };
+    napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

@@ -76,6 +76,34 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "", 
     return lib_path
 
 
+ADDON_SRC = PKG_DIR.parent / "native" / "rt_addon.c"
+ADDON_PATH = LIB_DIR / "rt_addon.node"
+NODE_INCLUDE = Path("/usr/include/node")
+
+
+def build_addon(force: bool = False, verbose: bool = False):
+    """The N-API addon: C against Node's node_api.h, linked to
+    librt_amd.so next to it. Returns its path, or None when Node's headers are
+    not installed (the addon is then simply not built)."""
+    if not (NODE_INCLUDE / "node_api.h").exists():
+        return None
+    lib = build_native()
+    if not force and ADDON_PATH.exists() and ADDON_PATH.stat().st_mtime >= max(
+            ADDON_SRC.stat().st_mtime, lib.stat().st_mtime, (INCLUDE / "rt_amd.h").stat().st_mtime):
+        return ADDON_PATH
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if not cc:
+        raise RuntimeError("no C compiler for the N-API addon")
+    tmp = ADDON_PATH.with_suffix(".node.tmp")
+    cmd = [cc, "-O2", "-fPIC", "-shared", "-Wall", "-DNODE_GYP_MODULE_NAME=rt_addon", f"-I{NODE_INCLUDE}",
+           f"-I{INCLUDE}", str(ADDON_SRC), "-o", str(tmp), f"-L{LIB_DIR}", "-lrt_amd", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, ADDON_PATH)
+    return ADDON_PATH
+
+
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()

@@ -1,0 +1,62 @@
+"""The N-API addon (mcp-raytracer_amd/native/rt_addon.c): the binding the
+reference's TypeScript host would load, driven from
+Node by tests/node/addon_render.js - this repo's harness, not reference code."""
+import json
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+JS = ROOT / "tests" / "node" / "addon_render.js"
+
+
+@pytest.fixture(scope="module")
+def addon(rt):
+    from raytracer_amd import _build
+    if not shutil.which("node"):
+        pytest.skip("node not installed")
+    path = _build.build_addon()
+    if path is None:
+        pytest.skip("node_api.h not installed")
+    return path
+
+
+def _node(*args):
+    r = subprocess.run(["node", str(JS), *map(str, args)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_addon_loads_and_builds_cameras(addon):
+    out = _node(addon, "info")
+    assert out["version"] >= 1
+    assert out["objects"] == 8
+    assert out["info"]["imageWidth"] == 40 and out["info"]["imageHeight"] == 40
+    assert out["info"]["lights"] == 1
+
+
+def test_addon_throws_reference_errors(addon):
+    msgs = _node(addon, "errors")
+    assert msgs[0] == "Material not found: nope"
+    assert msgs[1] == "Unknown object type: torus"
+    assert "camera" in msgs[2]
+
+
+@pytest.mark.gpu
+def test_addon_render_matches_python_binding(rt, addon, gpu, tmp_path):
+    """Two renderRegion calls into one SharedArrayBuffer (the worker split of
+    generateImageBuffer) give the library's full-frame image."""
+    out_bin = tmp_path / "frame.bin"
+    res = _node(addon, "render", out_bin)
+    W, H = res["width"], res["height"]
+    got = np.frombuffer(out_bin.read_bytes(), np.uint8).reshape(H, W, 3)
+    sd = rt.generate_scene_data({"type": "cornell"})
+    cam = rt.create_camera_from_scene_data(sd, {"width": 40, "samples": 8, "depth": 8, "aTolerance": 0})
+    ref = np.zeros((H, W, 3), np.uint8)
+    st = cam.render(ref)
+    assert np.array_equal(got, ref)
+    assert sum(s["pixels"] for s in res["stats"]) == st.pixels
+    assert sum(s["samples"]["total"] for s in res["stats"]) == st.samples["total"]
