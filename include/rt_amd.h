@@ -98,7 +98,10 @@ typedef struct {
 /* Work counters of an instrumented launch (SURVEY.md §8d algorithmic bytes). */
 enum {
     RT_CT_NODE = 0, RT_CT_SPHERE, RT_CT_QUAD, RT_CT_PLANE, RT_CT_MATERIAL, RT_CT_LIGHT_QUAD,
-    RT_CT_LIGHT_SPHERE, RT_CT_BOUNCES, RT_CT_DIFFUSE, RT_CT_SAMPLES, RT_CT_RAYS, RT_CT_WORDS
+    RT_CT_LIGHT_SPHERE, RT_CT_BOUNCES, RT_CT_DIFFUSE, RT_CT_SAMPLES, RT_CT_RAYS,
+    RT_CT_EXACT,       /* primitives whose exact fp64 test ran (fast/brute strategies) */
+    RT_CT_EXACT_WAVE,  /* wave-level executions of those exact tests */
+    RT_CT_WORDS
 };
 /* count_work == 2 (diagnostic): wave-cycles (s_memtime) per path-loop section,
  * summed over waves, at work_counters[RT_CT_WORDS + RT_PR_*]. */

@@ -61,7 +61,10 @@ enum { ST_PIXELS = 0, ST_SAMPLES, ST_SMIN, ST_SMAX, ST_BOUNCES, ST_BMIN, ST_BMAX
 // Instrumentation words (u64): the algorithmic-work counts of SURVEY.md §8d.
 enum {
     CT_NODE = 0, CT_SPHERE, CT_QUAD, CT_PLANE, CT_MATERIAL, CT_LIGHT_QUAD, CT_LIGHT_SPHERE,
-    CT_BOUNCES, CT_DIFFUSE, CT_SAMPLES, CT_RAYS, CT_WORDS
+    CT_BOUNCES, CT_DIFFUSE, CT_SAMPLES, CT_RAYS,
+    CT_EXACT,       // primitives whose exact fp64 test ran (per lane)
+    CT_EXACT_WAVE,  // exact-test blocks a wave executed (any lane), counted once per wave
+    CT_WORDS
 };
 enum : unsigned long long { ERR_NO_BACKGROUND = 1ull, ERR_EMIT_STACK = 2ull };
 // Diagnostic build (INSTR == 2): wave-cycles spent in each section of the path
@@ -530,6 +533,12 @@ __device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, flo
 }
 
 // Exact candidate t (reference arithmetic) of primitive p on (0.001, inf).
+__device__ __forceinline__ void count_exact(uint32_t* cnt) {
+    cnt[CT_EXACT]++;
+    const unsigned long long m = __ballot(1);
+    if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) cnt[CT_EXACT_WAVE]++;
+}
+
 template <class Real, bool COUNT>
 __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>& r, const FRay& f, float thi,
                                                Real& t, uint32_t* cnt) {
@@ -537,6 +546,7 @@ __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>
     if (p.type == PRIM_SPHERE) {
         if (COUNT) cnt[CT_SPHERE]++;
         if (!sphere_maybe(p, f, thi)) return false;
+        if (COUNT) count_exact(cnt);
         return sphere_t<Real>(p, r, K<Real>::TMIN, inf, t);
     }
     if (p.type == PRIM_QUAD) {
@@ -544,9 +554,11 @@ __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>
         const int code = aquad_code(p);
         if (code != 0) {
             if (!aquad_maybe(p, code, f.o, f.d, f.dn, thi)) return false;
+            if (COUNT) count_exact(cnt);
             return aquad_t<Real>(p, code, r.o, r.d, K<Real>::TMIN, inf, t);
         }
         if (!planar_maybe<true>(p, f, thi)) return false;
+        if (COUNT) count_exact(cnt);
         return planar_t<Real, true>(p, r, K<Real>::TMIN, inf, t);
     }
     if (COUNT) cnt[CT_PLANE]++;
@@ -911,7 +923,11 @@ __device__ __forceinline__ V3 pixel_center(const RtCamera& C, int i, int j) {
 
 template <class Real, bool EMIT>
 __device__ __forceinline__ void path_begin(const RtCamera& C, Path<EMIT>& P, V3 pc, uint32_t pix, uint32_t sample) {
+#ifndef RT_ABL_NORNGINIT  // diagnostic ablation builds only
     P.rng = rng_init(C.seed_mix, pix, sample);
+#else
+    P.rng += (uint64_t)pix * 0x9E3779B97F4A7C15ull + sample;
+#endif
     const V3 du = ld3(C.du), dv = ld3(C.dv), cen = ld3(C.center);
     V3 ps = pc;
     if (C.samples > 1.0) {
@@ -1394,7 +1410,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 r.y = c.y;
                 r.z = c.z;
                 r.w = __int_as_float(P.bounces);
+#ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
                 sb.rec[(size_t)s * sb.slots + slot] = r;
+#endif
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;
                     cnt[CT_BOUNCES] += (uint32_t)P.bounces;

@@ -10,9 +10,9 @@ res = collections.defaultdict(dict)
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
-        if "pt_render" not in r["Kernel_Name"]:
+        if not any(k in r["Kernel_Name"] for k in ("pt_render", "pt_chunk", "pt_accum")):
             continue
-        kn = r["Kernel_Name"].split("<")[1].split(">")[0]
+        kn = r["Kernel_Name"].split("(")[0].replace("void rt::", "")
         per[(kn, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     for (kn, _), cs in per.items():
         for c, v in cs.items():
