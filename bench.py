@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "fast", "reference"],
                     help="closest-hit strategy (all bit-identical; auto = brute force up to 16 primitives)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--count-sub", type=int, default=0,
+                    help="tile subsample of the work-counting launch (0 = auto: 16 above 1000 objects)")
     ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="JSON with measured HBM bytes per launch (from rocprofv3 --pmc)")
     args = ap.parse_args()
@@ -115,11 +117,16 @@ def main():
     # traversal (its counts equal the oracle's: test_work_counters_match_oracle).
     # Identical seeds => identical paths to every timed launch, whatever the
     # closest-hit strategy, so this is a fixed per-workload figure.
-    _, counters = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world,
-                                    stream=sptr, synchronize=True, count_work=True, traversal="reference")
+    # Large scenes count on a 1/count_sub tile subsample of this rank's tiles
+    # (SURVEY.md §8d's 1/16 pixel subsample) and scale to the launch.
+    sub = args.count_sub or (16 if cam.info["n_objects"] > 1000 else 1)
+    st_sub, counters = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world * sub,
+                                         stream=sptr, synchronize=True, count_work=True, traversal="reference")
     st, _ = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr,
                               synchronize=True)
     my_pixels = int(st.pixels)
+    scale = my_pixels / max(int(st_sub.pixels), 1)
+    counters = {k: v * scale for k, v in counters.items()}
     bytes_per_launch = algorithmic_bytes(counters, my_pixels)
 
     def step():
@@ -184,7 +191,7 @@ def main():
                     f"{args.seed:#x}; no datasets",
             "config": {"workload": f"{args.scene} {W}x{H} spp={args.spp} depth={args.depth}",
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "depth": args.depth,
-                       "precision": args.precision, "adaptive": False,
+                       "precision": args.precision, "adaptive": False, "count_subsample": sub,
                        "traversal": ["fast", "reference", "brute"][cam.info["traversal"]],
                        "kernel": "chunked (lane work pool, in-order accumulate)" if accum_ms > 0
                                  else "sequential (wave per 8x8 tile)",

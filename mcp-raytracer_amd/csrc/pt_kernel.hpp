@@ -32,7 +32,7 @@
 
 namespace rt {
 
-// The scene lives in one device buffer ("blob"): [tnodes][tprims][prims][mats][lights][nodes],
+// The scene lives in one device buffer ("blob"): [tnodes][tprims][tsph][prims][mats][lights][nodes],
 // 16-byte aligned sections. When [tnodes][prims] fits, every workgroup copies
 // it into LDS (LDS-resident launch): traversal and primitive reads are LDS reads.
 struct DevScene {
@@ -40,13 +40,15 @@ struct DevScene {
     const RtPrim* __restrict__ prims;   // global, or LDS in an LDS-resident launch
     const RtPrim* __restrict__ gprims;  // always the global copy (scalar-load reads)
     const int32_t* __restrict__ tprims; // fast-traversal leaves -> primitive slots (LDS when resident)
+    const float4* __restrict__ tsph;    // per tprims entry: sphere {centre, fp32 radius} or NaNs (LDS when resident)
     const RtMat* __restrict__ mats;
     const RtLight* __restrict__ lights;
     const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
-    const uint4* __restrict__ blob;     // the whole scene: [tnodes][tprims][prims][mats][lights][nodes]
-    int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS ([tnodes][tprims][prims])
+    const uint4* __restrict__ blob;     // the whole scene: [tnodes][tprims][tsph][prims][mats][lights][nodes]
+    int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS ([tnodes][tprims][tsph][prims])
     int32_t off_prims;                  // byte offset of prims in the blob
     int32_t off_tprims;                 // byte offset of tprims in the blob
+    int32_t off_tsph;                   // byte offset of tsph in the blob
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
@@ -484,10 +486,10 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 }
 
 // fp32 pre-filters: false only when the exact test surely gives no t <= thi.
-__device__ __forceinline__ bool sphere_maybe(const RtPrim& p, const FRay& f, float thi) {
-    const float ox = f.o[0] - p.g0[0], oy = f.o[1] - p.g0[1], oz = f.o[2] - p.g0[2];  // = the reference's oc
+__device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi) {
+    const float ox = f.o[0] - g.x, oy = f.o[1] - g.y, oz = f.o[2] - g.z;  // = the reference's oc
     const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
-    const float r = p.g0[3];
+    const float r = g.w;
     const float oo = ox * ox + oy * oy + oz * oz;
     const float disc = b * b - f.a * (oo - r * r);
     // every term of disc is bounded by a*(|oc|^2 + r^2) (b^2 <= a|oc|^2); the
@@ -545,7 +547,7 @@ __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>
     const Real inf = (Real)__builtin_inf();
     if (p.type == PRIM_SPHERE) {
         if (COUNT) cnt[CT_SPHERE]++;
-        if (!sphere_maybe(p, f, thi)) return false;
+        if (!sphere_maybe(make_float4(p.g0[0], p.g0[1], p.g0[2], p.g0[3]), f, thi)) return false;
         if (COUNT) count_exact(cnt);
         return sphere_t<Real>(p, r, K<Real>::TMIN, inf, t);
     }
@@ -599,9 +601,21 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             const int first = v >> 3;
             const int end = first + (v & 7);
             for (int m = first; m < end; ++m) {
-                const int k = S.tprims[m];  // reference leaf slot (the tie-break key)
+                const float4 g = S.tsph[m];
                 Real t;
-                if (prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt) && (t < best_t || (t == best_t && k < best))) {
+                int k;  // reference leaf slot (the tie-break key)
+                bool cand;
+                if (g.w == g.w) {  // sphere: pre-filter from the compact leaf-order record
+                    if (COUNT) cnt[CT_SPHERE]++;
+                    if (!sphere_maybe(g, f, thi)) continue;
+                    if (COUNT) count_exact(cnt);
+                    k = S.tprims[m];
+                    cand = sphere_t<Real>(S.prims[k], r, K<Real>::TMIN, (Real)__builtin_inf(), t);
+                } else {
+                    k = S.tprims[m];
+                    cand = prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt);
+                }
+                if (cand && (t < best_t || (t == best_t && k < best))) {
                     best_t = t;
                     best = k;
                     thi = upper_f<Real>(t);
@@ -1161,6 +1175,7 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
         const char* b = reinterpret_cast<const char*>(dst);
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
+        S.tsph = reinterpret_cast<const float4*>(b + S0.off_tsph);
         S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
     }
     return S;

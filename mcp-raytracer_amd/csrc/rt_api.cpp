@@ -70,7 +70,7 @@ struct rt_camera {
     int device = -1;
     uint4* d_blob = nullptr;  // [tnodes][prims][mats][lights][nodes] (DevScene)
     int32_t lds_words = 0;    // [tnodes][prims] prefix, 16-byte words
-    int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0;
+    int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // path start, path end, accumulate end
     bool ev_recorded = false, ev_accum = false;
@@ -116,6 +116,7 @@ struct rt_camera {
         std::vector<char> blob;
         append(blob, build.tnodes, nullptr);
         append(blob, build.tprims, &off_tprims);
+        append(blob, build.tsph, &off_tsph);
         append(blob, build.prims, &off_prims);
         lds_words = (int32_t)(blob.size() / 16);
         append(blob, build.mats, &off_mats);
@@ -157,6 +158,8 @@ struct rt_camera {
         S.gprims = S.prims;
         S.tprims = reinterpret_cast<const int32_t*>(b + off_tprims);
         S.off_tprims = off_tprims;
+        S.tsph = reinterpret_cast<const float4*>(b + off_tsph);
+        S.off_tsph = off_tsph;
         S.mats = reinterpret_cast<const RtMat*>(b + off_mats);
         S.lights = reinterpret_cast<const RtLight*>(b + off_lights);
         S.nodes = reinterpret_cast<const RtNode*>(b + off_nodes);
@@ -208,10 +211,13 @@ struct rt_camera {
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
         // Fixed spp: the chunked kernel balances small images (few tiles per
-        // resident wave) far better; large images already balance over tiles and
-        // skip the sample-buffer round trip.
+        // resident wave) far better; large images of LDS-resident scenes already
+        // balance over tiles and skip the sample-buffer round trip. Scenes
+        // traversed from global memory (long, variable per-sample cost: a tile
+        // waits for its slowest lane) take the chunked kernel at any size.
         const long resident_waves = (long)cus * (kBlockChunk / kWave);
-        const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 4 * resident_waves);
+        const bool big_scene = v.trav == TRAV_FAST && !g.lds_scene;
+        const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 4 * resident_waves || big_scene);
         if (C.adaptive || C.n_samples <= 0 || !chunked) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
             hip_check(hipEventRecord(ev[0], stream), "hipEventRecord");

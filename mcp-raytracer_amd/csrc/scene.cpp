@@ -1261,6 +1261,14 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
             b.out.tdepth = b.out.bvh_depth;
         }
         b.out.tprims.resize((b.out.tprims.size() + 3) / 4 * 4, 0);  // 16-byte blob sections
+        // leaf-order sphere records for the fp32 pre-filter: contiguous per leaf and
+        // a quarter of a primitive record, so large scenes stay cache-resident
+        b.out.tsph.assign(b.out.tprims.size() * 4, std::numeric_limits<float>::quiet_NaN());
+        for (size_t m = 0; m < b.out.tprims.size(); ++m) {
+            const RtPrim& p = b.out.prims[(size_t)b.out.tprims[m]];
+            if (p.type == PRIM_SPHERE)
+                for (int c = 0; c < 4; ++c) b.out.tsph[m * 4 + c] = p.g0[c];
+        }
     }
     cam.stack_depth = std::max(b.out.bvh_depth, b.out.tdepth) + 1;
     b.out.fast_ok = prims_inside_boxes(b.out.prims);

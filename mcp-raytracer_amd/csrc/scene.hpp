@@ -132,6 +132,7 @@ struct SceneBuild {
     std::vector<RtNode> fnodes;  // same tree, boxes for the fast traversal (padded / reject-marked)
     std::vector<RtTNode> tnodes; // fast-traversal tree, children-in-parent (SAH, or the reference tree)
     std::vector<int32_t> tprims; // its leaves' primitive slots (padded to a multiple of 4)
+    std::vector<float> tsph;     // per tprims entry: sphere {centre, fp32 radius}, NaNs for other types
     int32_t troot = 0;           // reference of the root (TNode index or leaf code)
     int tdepth = 0;              // its depth (root = 1)
     RtNode troot_box{};          // its root box (padded)

@@ -13,8 +13,11 @@ def main():
     import torch
     from bench import SCENES
     import raytracer_amd as rt
-    for scene, width, spp, depth, trav in [("cornell", 800, 64, 16, "brute"), ("cornell", 800, 64, 16, "fast"),
-                                           ("spheres", 800, 16, 8, "fast"), ("rain", 1920, 16, 16, "fast")]:
+    cfgs = [("cornell", 800, 64, 16, "brute"), ("cornell", 800, 64, 16, "fast"),
+            ("spheres", 800, 16, 8, "fast"), ("rain", 1920, 16, 16, "fast"), ("spheres100k", 1024, 4, 100, "fast")]
+    if len(sys.argv) > 1:
+        cfgs = [c for c in cfgs if c[0] in sys.argv[1:]]
+    for scene, width, spp, depth, trav in cfgs:
         cfg, extra = SCENES[scene]
         cam = rt.create_camera_from_scene_data(rt.generate_scene_data(cfg), {
             "width": width, "samples": spp, "depth": depth, "aTolerance": 0, "traversal": trav, **extra})

@@ -23,7 +23,7 @@ def main():
 
     cfgs = [("cornell", 800, 256, 16, "ref", "auto"), ("cornell", 800, 256, 16, "ref", "fast"),
             ("cornell", 800, 256, 16, "fp32", "auto"), ("spheres", 800, 64, 8, "ref", "auto"),
-            ("rain", 1920, 64, 16, "ref", "auto")]
+            ("rain", 1920, 64, 16, "ref", "auto"), ("spheres100k", 1024, 4, 100, "ref", "auto")]
     if len(sys.argv) > 1:
         cfgs = [c for c in cfgs if c[0] in sys.argv[1:]]
     for scene, width, spp, depth, prec, trav in cfgs:
