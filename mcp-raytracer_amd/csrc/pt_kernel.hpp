@@ -577,8 +577,50 @@ __device__ __forceinline__ float upper_f(Real t) {
 
 // `stk` / `stkt`: this lane's columns of the LDS node / entry-distance stacks.
 // Walks the children-in-parent tree (RtTNode): one 64-byte node read tests
-// both children; the nearer hit child is taken, the farther pushed with its
-// entry distance, and popped entries are culled against the best hit.
+// both children; the nearer hit child is taken, the farther pushed (with its
+// entry distance when kStackTnear, culled on pop against the best hit).
+//
+// Lanes of a wave reach leaves at different steps. RT_TRAV_WW (default) runs
+// node steps and leaf tests as two separate loops: a lane that reaches a leaf
+// parks it and keeps walking nodes until every lane still walking holds a
+// parked leaf, then the wave tests leaves together - otherwise nearly every
+// node step would also pay for some lane's (four times longer) leaf test.
+// Node steps taken while a leaf is parked cull with a possibly stale bound;
+// that only costs extra node tests (the answer is the (t, slot) minimum).
+#ifndef RT_TRAV_WW
+#define RT_TRAV_WW 1
+#endif
+constexpr int kTravDone = (int)0x80000000;  // no node / leaf (leaf refs are ~v, v < 2^31 - 1)
+
+template <class Real, bool COUNT>
+__device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
+                                          Real& best_t, int& best, uint32_t* cnt) {
+    const int v = ~ref;
+    const int first = v >> 3;
+    const int end = first + (v & 7);
+    for (int m = first; m < end; ++m) {
+        const float4 g = S.tsph[m];
+        Real t;
+        int k;  // reference leaf slot (the tie-break key)
+        bool cand;
+        if (g.w == g.w) {  // sphere: pre-filter from the compact leaf-order record
+            if (COUNT) cnt[CT_SPHERE]++;
+            if (!sphere_maybe(g, f, thi)) continue;
+            if (COUNT) count_exact(cnt);
+            k = S.tprims[m];
+            cand = sphere_t<Real>(S.prims[k], r, K<Real>::TMIN, (Real)__builtin_inf(), t);
+        } else {
+            k = S.tprims[m];
+            cand = prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt);
+        }
+        if (cand && (t < best_t || (t == best_t && k < best))) {
+            best_t = t;
+            best = k;
+            thi = upper_f<Real>(t);
+        }
+    }
+}
+
 template <class Real, bool COUNT>
 __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
                                                 float* stkt, uint32_t* cnt) {
@@ -592,65 +634,67 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
         t_hit = best_t;
         return -1;
     }
-    int ref = S.troot;
     int sp = 0;
-    while (true) {
-        bool next = false;
-        if (ref < 0) {
-            const int v = ~ref;
-            const int first = v >> 3;
-            const int end = first + (v & 7);
-            for (int m = first; m < end; ++m) {
-                const float4 g = S.tsph[m];
-                Real t;
-                int k;  // reference leaf slot (the tie-break key)
-                bool cand;
-                if (g.w == g.w) {  // sphere: pre-filter from the compact leaf-order record
-                    if (COUNT) cnt[CT_SPHERE]++;
-                    if (!sphere_maybe(g, f, thi)) continue;
-                    if (COUNT) count_exact(cnt);
-                    k = S.tprims[m];
-                    cand = sphere_t<Real>(S.prims[k], r, K<Real>::TMIN, (Real)__builtin_inf(), t);
-                } else {
-                    k = S.tprims[m];
-                    cand = prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt);
-                }
-                if (cand && (t < best_t || (t == best_t && k < best))) {
-                    best_t = t;
-                    best = k;
-                    thi = upper_f<Real>(t);
-                }
-            }
-        } else {
-            const RtTNode nd = S.tnodes[ref];
-            float ta, tb;
-            if (COUNT) cnt[CT_NODE] += 2;
-            const bool ha = slab(nd.box[0], f, thi, ta);
-            const bool hb = slab(nd.box[1], f, thi, tb);
-            if (ha && hb) {
-                const bool a_first = ta <= tb;
-                stk[sp * kStackStride] = a_first ? nd.box[1].a : nd.box[0].a;
-                if (kStackTnear) stkt[sp * kStackStride] = a_first ? tb : ta;
-                ++sp;
-                ref = a_first ? nd.box[0].a : nd.box[1].a;
-                next = true;
-            } else if (ha || hb) {
-                ref = ha ? nd.box[0].a : nd.box[1].a;
-                next = true;
-            }
+    // next stacked entry (kTravDone when the stack is empty)
+    auto pop = [&]() -> int {
+        while (sp > 0) {
+            --sp;
+            if (!kStackTnear || stkt[sp * kStackStride] <= thi) return stk[sp * kStackStride];
         }
-        if (!next) {
-            while (sp > 0) {
-                --sp;
-                if (!kStackTnear || stkt[sp * kStackStride] <= thi) {
-                    ref = stk[sp * kStackStride];
-                    next = true;
-                    break;
-                }
+        return kTravDone;
+    };
+    // one node step: the next node / leaf to visit
+    auto node_step = [&](int ref) -> int {
+        const RtTNode nd = S.tnodes[ref];
+        float ta, tb;
+        if (COUNT) cnt[CT_NODE] += 2;
+        const bool ha = slab(nd.box[0], f, thi, ta);
+        const bool hb = slab(nd.box[1], f, thi, tb);
+        if (ha && hb) {
+            const bool a_first = ta <= tb;
+            stk[sp * kStackStride] = a_first ? nd.box[1].a : nd.box[0].a;
+            if (kStackTnear) stkt[sp * kStackStride] = a_first ? tb : ta;
+            ++sp;
+            return a_first ? nd.box[0].a : nd.box[1].a;
+        }
+        if (ha || hb) return ha ? nd.box[0].a : nd.box[1].a;
+        return pop();
+    };
+    int ref = S.troot;
+#if RT_TRAV_WW
+    int leaf = kTravDone;  // parked leaf
+    while (ref != kTravDone || leaf != kTravDone) {
+        while (ref >= 0) {
+            ref = node_step(ref);
+            if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
+                leaf = ref;
+                ref = pop();
             }
-            if (!next) break;
+            if (__ballot(leaf == kTravDone) == 0ull) break;  // every walking lane holds a leaf
+        }
+        if (leaf == kTravDone && ref != kTravDone) {  // the walk stopped on a leaf (or started on one)
+            leaf = ref;
+            ref = pop();
+        }
+        while (leaf != kTravDone) {
+            leaf_test<Real, COUNT>(S, leaf, r, f, thi, best_t, best, cnt);
+            leaf = kTravDone;
+            if (ref < 0 && ref != kTravDone) {  // the walk also stopped on a leaf
+                leaf = ref;
+                ref = pop();
+            }
         }
     }
+#else
+    while (ref != kTravDone) {
+        if (ref < 0) {
+            leaf_test<Real, COUNT>(S, ref, r, f, thi, best_t, best, cnt);
+            ref = pop();
+        } else {
+            ref = node_step(ref);
+        }
+    }
+#endif
     t_hit = best_t;
     return best;
 }

@@ -9,4 +9,7 @@ for v in main $VARIANTS; do
   $B > gpurun_out/b_cornell_$v.log 2>&1 || exit $?
   $B --scene spheres --spp 64 --depth 8 > gpurun_out/b_spheres_$v.log 2>&1 || exit $?
   $B --scene rain --width 1920 --spp 128 --depth 16 --steps 3 > gpurun_out/b_rain_$v.log 2>&1 || exit $?
+  if [ -n "$BIG" ]; then
+    timeout -k 10 300 python bench.py --scene spheres100k --width 4096 --spp 16 --depth 100 --steps 2 --warmup 1 --no-cpu > gpurun_out/b_100k_$v.log 2>&1 || exit $?
+  fi
 done
