@@ -332,3 +332,52 @@ def test_chunked_kernel_equals_sequential(rt, gpu, name, monkeypatch):
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1], equal_nan=True)
     assert outs[0][2].samples == outs[1][2].samples and outs[0][2].bounces == outs[1][2].bounces
+
+
+def _tiny_scene(n):
+    objs = [{"type": "sphere", "pos": [0.9 * k - 0.9, 0.3 * (k % 2), -0.2 * k], "r": 0.45, "material": "m"}
+            for k in range(n)]
+    return {"camera": {"vfov": 40, "from": [0, 0.5, 4], "at": [0, 0, 0], "up": [0, 1, 0],
+                       "background": {"type": "gradient", "top": [0.5, 0.7, 1.0], "bottom": [1, 1, 1]}},
+            "materials": [{"id": "m", "material": {"type": "metal", "color": [0.8, 0.8, 0.8], "fuzz": 0.1}}],
+            "objects": objs}
+
+
+@pytest.mark.parametrize("n", [1, 3, 5])
+def test_tiny_scenes_every_strategy(rt, oracle, gpu, n):
+    """One-leaf trees (the fast walk starts on a leaf) and two-leaf trees: every
+    closest-hit strategy against the oracle, on hits and on images."""
+    sd = _tiny_scene(n)
+    rng = np.random.default_rng(n)
+    m = 3000
+    o = rng.uniform(-3, 3, (m, 3)).astype(np.float32)
+    d = rng.normal(size=(m, 3)).astype(np.float32)
+    c = _hit_equal(rt, oracle, sd, o, d)
+    assert (c[:, 0] > 0).any()
+    ro = {"width": 40, "samples": 4, "depth": 6, **NOADAPT}
+    orc = oracle.render(sd, ro)
+    for trav in ("fast", "brute", "reference"):
+        _, rgb, rad, _ = _render_gpu(rt, sd, {**ro, "traversal": trav})
+        rgb_eq, rad_eq, maxd = _agreement(rad, rgb, orc["radiance"], orc["rgb"])
+        assert rgb_eq >= 0.995 and rad_eq >= 0.995, (trav, rgb_eq, rad_eq, maxd)
+
+
+def test_large_scene_global_traversal(rt, oracle, gpu):
+    """A scene too large for the LDS-resident copy (deeper SAH tree walked from
+    global memory, chunked kernel): fast == reference traversal bit for bit,
+    and hits against the oracle."""
+    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 6000, "seed": 9}})
+    ro = {"width": 96, "aspect": 1, "samples": 8, "depth": 12, **NOADAPT}
+    outs = []
+    for trav in ("reference", "fast"):
+        cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
+        outs.append((rgb, rad, st))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1], equal_nan=True)
+    assert outs[0][2].bounces == outs[1][2].bounces
+    rng = np.random.default_rng(3)
+    n = 4000
+    o = (rng.uniform(-20, 20, (n, 3)) + np.float64([0, 2, 0])).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[:, 1] = -np.abs(d[:, 1])  # mostly toward the sphere field
+    _hit_equal(rt, oracle, sd, o, d, travs=("reference", "fast"))
