@@ -15,8 +15,8 @@ struct LaunchGeom {
     int tiles_x;
     int my_tiles;
     int grid;
-    size_t lds_bytes;  // traversal stack + (lds_scene) the scene blob
-    bool lds_scene;    // copy the scene into LDS (small scenes; never with the reference traversal)
+    size_t lds_bytes;  // traversal stack + the LDS-resident scene prefix
+    int lds_level;     // LDS-resident scene: 0 none, 1 traversal data + prims, 2 also mats + lights
 };
 
 // LDS budget (stack + [tnodes][prims]) up to which the scene is copied into LDS.

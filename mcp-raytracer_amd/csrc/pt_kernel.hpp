@@ -43,10 +43,14 @@ struct DevScene {
     const float4* __restrict__ tsph;    // per tprims entry: sphere {centre, fp32 radius} or NaNs (LDS when resident)
     const RtMat* __restrict__ mats;
     const RtLight* __restrict__ lights;
+    const RtLight* __restrict__ glights; // always the global copy (scalar-load reads)
     const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
     const uint4* __restrict__ blob;     // the whole scene: [tnodes][tprims][tsph][prims][mats][lights][nodes]
-    int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS ([tnodes][tprims][tsph][prims])
+    int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS (LDSS 1: [tnodes][tprims][tsph][prims],
+                                        // LDSS 2: also [mats][lights])
     int32_t off_prims;                  // byte offset of prims in the blob
+    int32_t off_mats;                   // byte offset of mats in the blob
+    int32_t off_lights;                 // byte offset of lights in the blob
     int32_t off_tprims;                 // byte offset of tprims in the blob
     int32_t off_tsph;                   // byte offset of tsph in the blob
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
@@ -1101,7 +1105,7 @@ __device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, 
                         const Real cv = cosine_value<Real>(b, gdir);
                         Real sum = (Real)0.5 * cv;
                         for (int l = 0; l < C.n_lights; ++l)
-                            sum += lw * light_pdf_value<Real, COUNT, true>(S, ld_uniform(S.lights, l), p, gdir, cnt);
+                            sum += lw * light_pdf_value<Real, COUNT, true>(S, ld_uniform(S.glights, l), p, gdir, cnt);
                         const Real pv = sum / total;
                         if (pv <= (Real)0.0001) {
                             term = true;
@@ -1207,12 +1211,16 @@ __device__ __forceinline__ void publish_counters(const RenderOut& out, const uin
     }
 }
 
-// Workgroup prologue shared by the render kernels: LDS-resident traversal data
+// Workgroup prologue shared by the render kernels: LDS-resident scene data
 // (one cooperative copy per workgroup) and this thread's stack columns.
-template <bool LDSS>
+// LDSS 0: all scene reads from global memory; 1: the traversal data and the
+// primitive records in LDS; 2: also the material and light tables. (Wave-
+// uniform reads - the brute-force primitive loop, the light list - stay on
+// scalar loads from the global copy.)
+template <int LDSS>
 __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
     DevScene S = S0;
-    if (LDSS) {
+    if (LDSS > 0) {
         uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
         for (int w = threadIdx.x; w < S0.lds_words; w += blockDim.x) dst[w] = S0.blob[w];
         __syncthreads();
@@ -1221,6 +1229,10 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
         S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
         S.tsph = reinterpret_cast<const float4*>(b + S0.off_tsph);
         S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
+        if (LDSS > 1) {
+            S.mats = reinterpret_cast<const RtMat*>(b + S0.off_mats);
+            S.lights = reinterpret_cast<const RtLight*>(b + S0.off_lights);
+        }
     }
     return S;
 }
@@ -1232,7 +1244,7 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
 // Kernel arguments: S0 must stay the first parameter (cam_opaque reads it at kernarg offset 0).
 // INSTR: 0 = product build, 1 = work counters, 2 = section timing.
 // ---------------------------------------------------------------------------
-template <class Real, bool EMIT, int INSTR, int TRAV, bool LDSS>
+template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
 __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion reg, RenderOut out,
                                                                          int tiles_x, int my_tiles) {
     constexpr bool COUNT = INSTR == 1;
@@ -1370,7 +1382,7 @@ __device__ __forceinline__ void item_pixel(const RtRegion& reg, int tiles_x, dou
     j = reg.y + ty * kTile + (l / kTile);
 }
 
-template <class Real, bool EMIT, int INSTR, int TRAV, bool LDSS>
+template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
 __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRegion reg, RenderOut out,
                                                                         int tiles_x, SampleBuf sb) {
     constexpr bool COUNT = INSTR == 1;

@@ -5,7 +5,7 @@
 
 namespace rt {
 
-template <bool EMIT, int INSTR, int TRAV, bool LDSS>
+template <bool EMIT, int INSTR, int TRAV, int LDSS>
 static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                       const SampleBuf* sb, hipStream_t stream) {
     if (sb)
@@ -20,8 +20,11 @@ static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& o
 template <bool EMIT, int INSTR, int TRAV>
 static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                      const SampleBuf* sb, hipStream_t stream) {
-    if (g.lds_scene && TRAV != TRAV_REFERENCE) return go2<EMIT, INSTR, TRAV, TRAV != TRAV_REFERENCE>(S, reg, out, g, sb, stream);
-    return go2<EMIT, INSTR, TRAV, false>(S, reg, out, g, sb, stream);
+    // LDS residency levels (pt_kernel.hpp scene_prologue); never with the reference traversal
+    constexpr int L1 = TRAV == TRAV_FAST ? 1 : 0, L2 = TRAV == TRAV_REFERENCE ? 0 : 2;
+    if (g.lds_level >= 2) return go2<EMIT, INSTR, TRAV, L2>(S, reg, out, g, sb, stream);
+    if (g.lds_level == 1) return go2<EMIT, INSTR, TRAV, L1>(S, reg, out, g, sb, stream);
+    return go2<EMIT, INSTR, TRAV, 0>(S, reg, out, g, sb, stream);
 }
 
 template <int TRAV>

@@ -69,7 +69,8 @@ struct rt_camera {
 
     int device = -1;
     uint4* d_blob = nullptr;  // [tnodes][prims][mats][lights][nodes] (DevScene)
-    int32_t lds_words = 0;    // [tnodes][prims] prefix, 16-byte words
+    int32_t lds_words = 0;    // [tnodes][tprims][tsph][prims] prefix, 16-byte words
+    int32_t lds_words2 = 0;   // the same + [mats][lights]
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // path start, path end, accumulate end
@@ -121,6 +122,7 @@ struct rt_camera {
         lds_words = (int32_t)(blob.size() / 16);
         append(blob, build.mats, &off_mats);
         append(blob, build.lights, &off_lights);
+        lds_words2 = (int32_t)(blob.size() / 16);
         append(blob, build.nodes, &off_nodes);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
         if (!blob.empty()) hip_check(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice), "hipMemcpy");
@@ -162,10 +164,13 @@ struct rt_camera {
         S.off_tsph = off_tsph;
         S.mats = reinterpret_cast<const RtMat*>(b + off_mats);
         S.lights = reinterpret_cast<const RtLight*>(b + off_lights);
+        S.glights = S.lights;
         S.nodes = reinterpret_cast<const RtNode*>(b + off_nodes);
         S.blob = d_blob;
         S.lds_words = lds_words;
         S.off_prims = off_prims;
+        S.off_mats = off_mats;
+        S.off_lights = off_lights;
         S.lds_stack_bytes = 0;
         S.troot = build.troot;
         S.root_box = build.troot_box;
@@ -196,12 +201,18 @@ struct rt_camera {
         g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus));  // one persistent workgroup per CU
         const KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
         const size_t stack = stack_lds_bytes(C.stack_depth, v.trav);
-        // LDS copy for the BVH walk only: the brute-force loop reads its (wave-
-        // uniform) primitive records through scalar loads, which keeps the
-        // per-primitive control flow scalar.
-        g.lds_scene = lds_scene_enabled() && v.trav == TRAV_FAST &&
-                      stack + (size_t)lds_words * 16 <= (size_t)std::min(lds_max, kLdsSceneMaxBytes);
-        g.lds_bytes = stack + (g.lds_scene ? (size_t)lds_words * 16 : 0);
+        // LDS-resident scene: the BVH walk's data and the primitive records
+        // (level 1), plus the material and light tables when they fit too
+        // (level 2). The brute-force loop reads its wave-uniform primitive
+        // records through scalar loads either way; LDS serves the per-lane
+        // reads (hit record, materials, light sampling).
+        const size_t lds_cap = (size_t)std::min(lds_max, kLdsSceneMaxBytes);
+        g.lds_level = 0;
+        if (lds_scene_enabled() && v.trav != TRAV_REFERENCE) {
+            if (stack + (size_t)lds_words2 * 16 <= lds_cap && env_flag("RT_AMD_LDS_MATS", true)) g.lds_level = 2;
+            else if (v.trav == TRAV_FAST && stack + (size_t)lds_words * 16 <= lds_cap) g.lds_level = 1;
+        }
+        g.lds_bytes = stack + (size_t)(g.lds_level == 2 ? lds_words2 : g.lds_level == 1 ? lds_words : 0) * 16;
         if (g.lds_bytes > (size_t)lds_max)
             throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile};
@@ -210,13 +221,14 @@ struct rt_camera {
         if (mine == 0) return;
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
+        S.lds_words = g.lds_level == 2 ? lds_words2 : lds_words;
         // Fixed spp: the chunked kernel balances small images (few tiles per
         // resident wave) far better; large images of LDS-resident scenes already
         // balance over tiles and skip the sample-buffer round trip. Scenes
         // traversed from global memory (long, variable per-sample cost: a tile
         // waits for its slowest lane) take the chunked kernel at any size.
         const long resident_waves = (long)cus * (kBlockChunk / kWave);
-        const bool big_scene = v.trav == TRAV_FAST && !g.lds_scene;
+        const bool big_scene = v.trav == TRAV_FAST && g.lds_level == 0;
         const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 4 * resident_waves || big_scene);
         if (C.adaptive || C.n_samples <= 0 || !chunked) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
