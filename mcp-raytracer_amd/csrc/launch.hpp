@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "pt_kernel.hpp"
 
 namespace rt {
@@ -43,9 +45,12 @@ hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* coun
 hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float* orig, const float* dir,
                                 double* out, hipStream_t stream);
 
-// LDS bytes per 256-thread block for the traversal stack.
-inline size_t stack_lds_bytes(int stack_depth, int trav) {
-    if (trav == TRAV_BRUTE) return 0;
+// LDS bytes per workgroup for the traversal stack (fast / reference) or the
+// per-lane candidate bounds of the nearest-first brute force.
+inline size_t stack_lds_bytes(int stack_depth, int trav, int n_prims) {
+    if (trav == TRAV_BRUTE)  // larger forced brute-force scenes take the in-order loop (no LDS)
+        return RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims ? (size_t)std::max(n_prims, 1) * kStackStride * sizeof(float)
+                                                           : 0;
     const size_t d = (size_t)(stack_depth > 0 ? stack_depth : 1);
     return d * kStackStride * ((trav == TRAV_FAST && kStackTnear) ? 2 * sizeof(int) : sizeof(int));
 }

@@ -94,7 +94,7 @@ struct RenderOut {
 // Closest-hit strategies; all return the reference's hit bit-for-bit (see the
 // functions below). AUTO is resolved on the host.
 enum Traversal : int32_t { TRAV_FAST = 0, TRAV_REFERENCE = 1, TRAV_BRUTE = 2, TRAV_AUTO = 3 };
-constexpr int kBruteMaxPrims = 16;  // AUTO picks BRUTE up to this many primitives
+constexpr int kBruteMaxPrims = 16;  // AUTO picks BRUTE up to this many primitives (nearest-first form: <= 32)
 
 // Minimum waves per SIMD the path kernel is register-allocated for
 // (__launch_bounds__ second argument): 3 => <= 168 VGPRs.
@@ -320,12 +320,15 @@ __device__ __forceinline__ bool aquad_t_c(const RtPrim& p, V3 o3, V3 d3, Real tm
 
 // fp32 pre-filter of aquad_t_c: false only when the exact test surely rejects or
 // gives no t <= thi.
+// `lo` (all pre-filters): a lower bound of the exact t the test can return.
 template <int CODE>
-__device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, const float* d, float dn, float thi) {
+__device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, const float* d, float dn, float thi,
+                                              float& lo) {
     constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
     constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
     const float na = p.g3[a];
     const float denom = na * d[a];
+    lo = kTminLo;
     if (!(::fabsf(denom) > 1e-3f * dn)) return true;  // near-parallel: decide exactly
     const float no = na * o[a];
     const float D = p.g0[3];
@@ -333,6 +336,7 @@ __device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, c
     const float t = (D - no) * idn;
     const float et = kRel * ((::fabsf(D) + ::fabsf(no)) * ::fabsf(idn) + 2.0f * ::fabsf(t)) + 1e-30f;
     if (t + et < kTminLo || t - et > thi) return false;
+    lo = t - et;
     const float ph1 = o[ia] + t * d[ia] - p.g0[ia];
     const float ph2 = o[ib] + t * d[ib] - p.g0[ib];
     const float alpha = p.g3[3] * (ph1 * p.g2[3]);
@@ -357,15 +361,51 @@ __device__ __forceinline__ bool aquad_t(const RtPrim& p, int code, V3 o, V3 d, R
     }
 }
 __device__ __forceinline__ bool aquad_maybe(const RtPrim& p, int code, const float* o, const float* d, float dn,
-                                            float thi) {
+                                            float thi, float& lo) {
     switch (code) {
-        case 1: return aquad_maybe_c<1>(p, o, d, dn, thi);
-        case 2: return aquad_maybe_c<2>(p, o, d, dn, thi);
-        case 3: return aquad_maybe_c<3>(p, o, d, dn, thi);
-        case 4: return aquad_maybe_c<4>(p, o, d, dn, thi);
-        case 5: return aquad_maybe_c<5>(p, o, d, dn, thi);
-        default: return aquad_maybe_c<6>(p, o, d, dn, thi);
+        case 1: return aquad_maybe_c<1>(p, o, d, dn, thi, lo);
+        case 2: return aquad_maybe_c<2>(p, o, d, dn, thi, lo);
+        case 3: return aquad_maybe_c<3>(p, o, d, dn, thi, lo);
+        case 4: return aquad_maybe_c<4>(p, o, d, dn, thi, lo);
+        case 5: return aquad_maybe_c<5>(p, o, d, dn, thi, lo);
+        default: return aquad_maybe_c<6>(p, o, d, dn, thi, lo);
     }
+}
+
+// aquad_t_c with the axis code as a runtime value (one code path for lanes
+// testing different walls): the same operations on the same operands.
+__device__ __forceinline__ float sel3(float x, float y, float z, int i) { return i == 0 ? x : (i == 1 ? y : z); }
+constexpr uint32_t aquad_axes(int field) {  // 2-bit fields per code 1..6: a, ia, ib
+    uint32_t m = 0;
+    for (int c = 1; c <= 6; ++c) {
+        const int a = (c - 1) % 3, vflag = (c - 1) / 3;
+        const int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+        m |= (uint32_t)(field == 0 ? a : field == 1 ? ia : ib) << (2 * c);
+    }
+    return m;
+}
+template <class Real>
+__device__ __forceinline__ bool aquad_t_rt(const RtPrim& p, int code, V3 o3, V3 d3, Real tmin, Real tmax, Real& t) {
+    const int a = (int)((aquad_axes(0) >> (2 * code)) & 3u);
+    const int ia = (int)((aquad_axes(1) >> (2 * code)) & 3u);
+    const int ib = (int)((aquad_axes(2) >> (2 * code)) & 3u);
+    const float oa = sel3(o3.x, o3.y, o3.z, a), da = sel3(d3.x, d3.y, d3.z, a);
+    const float o1 = sel3(o3.x, o3.y, o3.z, ia), d1 = sel3(d3.x, d3.y, d3.z, ia);
+    const float o2 = sel3(o3.x, o3.y, o3.z, ib), d2 = sel3(d3.x, d3.y, d3.z, ib);
+    if (!(::isfinite(o1) && ::isfinite(d1) && ::isfinite(o2) && ::isfinite(d2))) return false;
+    const Real na = (Real)sel3(p.g3[0], p.g3[1], p.g3[2], a);
+    const Real denom = na * (Real)da;
+    if (m_abs(denom) < (Real)1e-8) return false;
+    const Real tt = (plane_d<Real>(p) - na * (Real)oa) / denom;
+    if (!(tmin < tt && tt < tmax)) return false;
+    const float ph1 = (o1 + (float)((Real)d1 * tt)) - sel3(p.g0[0], p.g0[1], p.g0[2], ia);
+    const float ph2 = (o2 + (float)((Real)d2 * tt)) - sel3(p.g0[0], p.g0[1], p.g0[2], ib);
+    const Real sw = (Real)p.g3[3];
+    const Real alpha = sw * (Real)(ph1 * p.g2[3]);
+    const Real beta = sw * (Real)(ph2 * p.g1[3]);
+    if (alpha < (Real)0 || alpha > (Real)1 || beta < (Real)0 || beta > (Real)1) return false;
+    t = tt;
+    return true;
 }
 __device__ __forceinline__ int aquad_code(const RtPrim& p) { return __float_as_int(p.g4[3]); }
 
@@ -490,7 +530,7 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 }
 
 // fp32 pre-filters: false only when the exact test surely gives no t <= thi.
-__device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi) {
+__device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi, float& lo) {
     const float ox = f.o[0] - g.x, oy = f.o[1] - g.y, oz = f.o[2] - g.z;  // = the reference's oc
     const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
     const float r = g.w;
@@ -503,14 +543,17 @@ __device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi)
     const float sq = __builtin_amdgcn_sqrtf(::fmaxf(disc, 0.0f) + tol) * (1.0f + kRel);
     const float et = kRel * (__builtin_amdgcn_sqrtf(oo * f.a) + ::fabsf(b) + sq) * f.ia + 1e-30f;
     if ((-b + sq) * f.ia * (1.0f + kRel) + et < kTminLo) return false;
-    if ((-b - sq) * f.ia * (1.0f - kRel) - et > thi) return false;
+    const float r1 = (-b - sq) * f.ia;
+    lo = r1 - ::fabsf(r1) * kRel - et;  // <= the first root; the second is larger
+    if (lo > thi) return false;
     return true;
 }
 
 template <bool QUAD>
-__device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, float thi) {
+__device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, float thi, float& lo) {
     const float nx = p.g3[0], ny = p.g3[1], nz = p.g3[2];
     const float denom = nx * f.d[0] + ny * f.d[1] + nz * f.d[2];
+    lo = kTminLo;
     if (!(::fabsf(denom) > 1e-3f * f.dn)) return true;  // near-parallel: decide exactly
     const float no = nx * f.o[0] + ny * f.o[1] + nz * f.o[2];
     const float D = p.g0[3];
@@ -520,6 +563,7 @@ __device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, flo
     const float et = (kRel * (::fabsf(D) + f.on) + 2.0f * kRel * f.dn * ::fabsf(t)) * ::fabsf(idn) +
                      kRel * ::fabsf(t) + 1e-30f;
     if (t + et < kTminLo || t - et > thi) return false;
+    lo = t - et;
     if (!QUAD) return true;
     const float px = f.o[0] + t * f.d[0] - p.g0[0];
     const float py = f.o[1] + t * f.d[1] - p.g0[1];
@@ -549,9 +593,10 @@ template <class Real, bool COUNT>
 __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>& r, const FRay& f, float thi,
                                                Real& t, uint32_t* cnt) {
     const Real inf = (Real)__builtin_inf();
+    float lo;
     if (p.type == PRIM_SPHERE) {
         if (COUNT) cnt[CT_SPHERE]++;
-        if (!sphere_maybe(make_float4(p.g0[0], p.g0[1], p.g0[2], p.g0[3]), f, thi)) return false;
+        if (!sphere_maybe(make_float4(p.g0[0], p.g0[1], p.g0[2], p.g0[3]), f, thi, lo)) return false;
         if (COUNT) count_exact(cnt);
         return sphere_t<Real>(p, r, K<Real>::TMIN, inf, t);
     }
@@ -559,16 +604,16 @@ __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>
         if (COUNT) cnt[CT_QUAD]++;
         const int code = aquad_code(p);
         if (code != 0) {
-            if (!aquad_maybe(p, code, f.o, f.d, f.dn, thi)) return false;
+            if (!aquad_maybe(p, code, f.o, f.d, f.dn, thi, lo)) return false;
             if (COUNT) count_exact(cnt);
             return aquad_t<Real>(p, code, r.o, r.d, K<Real>::TMIN, inf, t);
         }
-        if (!planar_maybe<true>(p, f, thi)) return false;
+        if (!planar_maybe<true>(p, f, thi, lo)) return false;
         if (COUNT) count_exact(cnt);
         return planar_t<Real, true>(p, r, K<Real>::TMIN, inf, t);
     }
     if (COUNT) cnt[CT_PLANE]++;
-    if (!planar_maybe<false>(p, f, thi)) return false;
+    if (!planar_maybe<false>(p, f, thi, lo)) return false;
     return planar_t<Real, false>(p, r, K<Real>::TMIN, inf, t);
 }
 
@@ -609,7 +654,8 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
         bool cand;
         if (g.w == g.w) {  // sphere: pre-filter from the compact leaf-order record
             if (COUNT) cnt[CT_SPHERE]++;
-            if (!sphere_maybe(g, f, thi)) continue;
+            float lo;
+            if (!sphere_maybe(g, f, thi, lo)) continue;
             if (COUNT) count_exact(cnt);
             k = S.tprims[m];
             cand = sphere_t<Real>(S.prims[k], r, K<Real>::TMIN, (Real)__builtin_inf(), t);
@@ -721,6 +767,90 @@ __device__ __forceinline__ int closest_hit_brute(const DevScene& S, int n_prims,
         if (prim_candidate<Real, COUNT>(p, r, f, thi, t, cnt) && t < best_t) {
             best_t = t;
             best = k;
+            thi = upper_f<Real>(t);
+        }
+    }
+    t_hit = best_t;
+    return best;
+}
+
+// Nearest-first brute force (RT_BRUTE_DEFER). The loop above runs primitive
+// k's exact test whenever ANY lane of the wave needs it - lanes hit different
+// walls, so a wave executes nearly every primitive's exact test per ray while
+// each lane needs about one. Here pass 1 (wave-uniform, scalar primitive
+// loads) only runs the fp32 pre-filters and keeps, per lane, the candidate set
+// and each candidate's lower bound on t (in this lane's LDS column `lot`).
+// Pass 2 exact-tests each lane's candidates nearest-first through one
+// type-generic code path per primitive type, and stops once the nearest
+// remaining lower bound lies beyond the best hit. Same (t, slot) minimum.
+#ifndef RT_BRUTE_DEFER
+#define RT_BRUTE_DEFER 1
+#endif
+template <bool COUNT>
+__device__ __forceinline__ bool prim_maybe(const RtPrim& p, const FRay& f, float& lo, uint32_t* cnt) {
+    const float thi = __builtin_inff();
+    if (p.type == PRIM_SPHERE) {
+        if (COUNT) cnt[CT_SPHERE]++;
+        return sphere_maybe(make_float4(p.g0[0], p.g0[1], p.g0[2], p.g0[3]), f, thi, lo);
+    }
+    if (p.type == PRIM_QUAD) {
+        if (COUNT) cnt[CT_QUAD]++;
+        const int code = aquad_code(p);
+        if (code != 0) return aquad_maybe(p, code, f.o, f.d, f.dn, thi, lo);
+        return planar_maybe<true>(p, f, thi, lo);
+    }
+    if (COUNT) cnt[CT_PLANE]++;
+    return planar_maybe<false>(p, f, thi, lo);
+}
+
+// The reference's exact t of primitive p on (0.001, inf); per-lane p.
+template <class Real>
+__device__ __forceinline__ bool prim_exact(const RtPrim& p, const RayK<Real>& r, Real& t) {
+    const Real inf = (Real)__builtin_inf();
+    if (p.type == PRIM_SPHERE) return sphere_t<Real>(p, r, K<Real>::TMIN, inf, t);
+    if (p.type == PRIM_QUAD) {
+        const int code = aquad_code(p);
+        if (code != 0) return aquad_t_rt<Real>(p, code, r.o, r.d, K<Real>::TMIN, inf, t);
+        return planar_t<Real, true>(p, r, K<Real>::TMIN, inf, t);
+    }
+    return planar_t<Real, false>(p, r, K<Real>::TMIN, inf, t);
+}
+
+template <class Real, bool COUNT>
+__device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
+                                                    float* lot, uint32_t* cnt) {
+    const FRay f = make_fray(r.o, r.d);
+    uint32_t mask = 0u;
+    for (int k = 0; k < n_prims; ++k) {
+        const RtPrim p = ld_uniform(S.gprims, k);
+        float lo;
+        if (prim_maybe<COUNT>(p, f, lo, cnt)) {
+            lot[k * kStackStride] = lo;
+            mask |= 1u << k;
+        }
+    }
+    Real best_t = (Real)__builtin_inf();
+    int best = -1;
+    float thi = __builtin_inff();
+    while (mask != 0u) {
+        // nearest remaining candidate (a NaN bound is never skipped: it is tested exactly)
+        int kb = __builtin_ctz(mask);
+        float lb = lot[kb * kStackStride];
+        for (uint32_t m = mask & (mask - 1u); m != 0u; m &= m - 1u) {
+            const int k = __builtin_ctz(m);
+            const float l = lot[k * kStackStride];
+            if (l < lb) {
+                lb = l;
+                kb = k;
+            }
+        }
+        if (lb > thi) break;  // every remaining candidate's t exceeds the best hit
+        mask &= ~(1u << kb);
+        if (COUNT) count_exact(cnt);
+        Real t;
+        if (prim_exact<Real>(S.prims[kb], r, t) && (t < best_t || (t == best_t && kb < best))) {
+            best_t = t;
+            best = kb;
             thi = upper_f<Real>(t);
         }
     }
@@ -945,7 +1075,11 @@ __device__ __forceinline__ const RtCamera& cam_opaque() {
 template <class Real, bool COUNT, int TRAV>
 __device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t, int* stk,
                                                float* stkt, uint32_t* cnt) {
-    if (TRAV == TRAV_BRUTE) return closest_hit_brute<Real, COUNT>(S, n_prims, r, t, cnt);
+    if (TRAV == TRAV_BRUTE) {
+        if (RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims)
+            return closest_hit_brute_nf<Real, COUNT>(S, n_prims, r, t, reinterpret_cast<float*>(stk), cnt);
+        return closest_hit_brute<Real, COUNT>(S, n_prims, r, t, cnt);
+    }
     if (TRAV == TRAV_FAST) return closest_hit_fast<Real, COUNT>(S, r, t, stk, stkt, cnt);
     return closest_hit<Real, COUNT>(S, r, t, stk, cnt);
 }

@@ -152,7 +152,8 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
 hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float* orig, const float* dir,
                                 double* out, hipStream_t stream) {
     const int grid = (n + kBlock - 1) / kBlock;
-    const size_t lds = stack_lds_bytes(S.cam.stack_depth, TRAV_FAST);  // largest footprint
+    const size_t lds = std::max(stack_lds_bytes(S.cam.stack_depth, TRAV_FAST, S.cam.n_prims),
+                                stack_lds_bytes(S.cam.stack_depth, TRAV_BRUTE, S.cam.n_prims));  // largest footprint
     if (trav == TRAV_BRUTE)
         hipLaunchKernelGGL(world_hit_kernel<TRAV_BRUTE>, dim3(grid), dim3(kBlock), lds, stream, S, n, orig, dir, out);
     else if (trav == TRAV_FAST)

@@ -200,7 +200,7 @@ struct rt_camera {
         const long want = (mine + (kBlock / kWave) - 1) / (kBlock / kWave);
         g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus));  // one persistent workgroup per CU
         const KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
-        const size_t stack = stack_lds_bytes(C.stack_depth, v.trav);
+        const size_t stack = stack_lds_bytes(C.stack_depth, v.trav, C.n_prims);
         // LDS-resident scene: the BVH walk's data and the primitive records
         // (level 1), plus the material and light tables when they fit too
         // (level 2). The brute-force loop reads its wave-uniform primitive
