@@ -45,6 +45,9 @@ struct DevScene {
     const RtLight* __restrict__ lights;
     const RtLight* __restrict__ glights; // always the global copy (scalar-load reads)
     const RtNode* __restrict__ nodes;   // the reference's boxes (reference traversal)
+    const RtOnb* __restrict__ onbs;     // [slot][precision][face] for slots < n_onb (LDS at level 2)
+    int32_t n_onb;                      // planar primitives' ONB table covers slots [0, n_onb)
+    int32_t off_onbs;                   // byte offset of onbs in the blob
     const uint4* __restrict__ blob;     // the whole scene: [tnodes][tprims][tsph][prims][mats][lights][nodes]
     int32_t lds_words;                  // 16-byte words of the blob prefix copied to LDS (LDSS 1: [tnodes][tprims][tsph][prims],
                                         // LDSS 2: also [mats][lights])
@@ -1215,7 +1218,15 @@ __device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, 
                     } else {
                         if (COUNT) cnt[CT_DIFFUSE]++;
                         // MixturePDF([CosinePDF(n), light pdfs...], [0.5, 0.5/nL...])
-                        const Onb b = make_onb<Real>(nrm);
+                        Onb b;
+                        if (pr.type != PRIM_SPHERE && h < S.n_onb) {
+                            const RtOnb& ob = S.onbs[(h * 2 + (sizeof(Real) == 4 ? 1 : 0)) * 2 + (front ? 0 : 1)];
+                            b.u = ld3(ob.u);
+                            b.v = ld3(ob.v);
+                            b.w = ld3(ob.w);
+                        } else {
+                            b = make_onb<Real>(nrm);
+                        }
                         const Real total = (Real)S.mix_total;
                         const Real lw = (Real)S.light_w;
                         const Real rnd = uniform<Real>(P.rng) * total;
@@ -1366,6 +1377,7 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
         if (LDSS > 1) {
             S.mats = reinterpret_cast<const RtMat*>(b + S0.off_mats);
             S.lights = reinterpret_cast<const RtLight*>(b + S0.off_lights);
+            S.onbs = reinterpret_cast<const RtOnb*>(b + S0.off_onbs);
         }
     }
     return S;

@@ -60,6 +60,38 @@ int device_cus(int dev) {
 
 }  // namespace
 
+// ONBasis of a hit normal (src/geometry/onbasis.ts:18-51), host side: the same
+// rt_math.hpp operations as the kernel's make_onb, so the stored basis equals
+// the one the kernel would build (ref: fp64 scalars, -ffp-contract=off).
+template <class Real>
+static RtOnb host_onb(V3 n) {
+    const V3 w = unit<Real>(n);
+    const V3 a = std::fabs((Real)w.x) > (Real)0.9 ? v3(0, 1, 0) : v3(1, 0, 0);
+    const V3 v = unit<Real>(cross<Real>(w, a));
+    const V3 u = cross<Real>(w, v);
+    return RtOnb{{u.x, u.y, u.z, 0.f}, {v.x, v.y, v.z, 0.f}, {w.x, w.y, w.z, 0.f}};
+}
+
+// Per planar primitive slot: [precision ref, fp32][face front, back] bases of
+// its hit normals (front: the plane normal; back: Vec3.negate of it). Covers
+// slots [0, last planar slot]; empty when the scene has no quad or plane.
+static std::vector<RtOnb> planar_onbs(const std::vector<RtPrim>& prims, int32_t* n_onb) {
+    int32_t n = 0;
+    for (size_t k = 0; k < prims.size(); ++k)
+        if (prims[k].type != PRIM_SPHERE) n = (int32_t)k + 1;
+    std::vector<RtOnb> t((size_t)n * 4, RtOnb{});
+    for (int32_t k = 0; k < n; ++k) {
+        if (prims[k].type == PRIM_SPHERE) continue;
+        const V3 pn = v3(prims[k].g3[0], prims[k].g3[1], prims[k].g3[2]);
+        t[k * 4 + 0] = host_onb<double>(pn);
+        t[k * 4 + 1] = host_onb<double>(neg(pn));
+        t[k * 4 + 2] = host_onb<float>(pn);
+        t[k * 4 + 3] = host_onb<float>(neg(pn));
+    }
+    *n_onb = n;
+    return t;
+}
+
 struct rt_camera {
     SceneBuild build;
     int32_t precision = PREC_REF;
@@ -71,7 +103,8 @@ struct rt_camera {
     uint4* d_blob = nullptr;  // [tnodes][prims][mats][lights][nodes] (DevScene)
     int32_t lds_words = 0;    // [tnodes][tprims][tsph][prims] prefix, 16-byte words
     int32_t lds_words2 = 0;   // the same + [mats][lights]
-    int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0;
+    int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
+    int32_t n_onb = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // path start, path end, accumulate end
     bool ev_recorded = false, ev_accum = false;
@@ -122,6 +155,8 @@ struct rt_camera {
         lds_words = (int32_t)(blob.size() / 16);
         append(blob, build.mats, &off_mats);
         append(blob, build.lights, &off_lights);
+        const std::vector<RtOnb> onbs = planar_onbs(build.prims, &n_onb);
+        append(blob, onbs, &off_onbs);
         lds_words2 = (int32_t)(blob.size() / 16);
         append(blob, build.nodes, &off_nodes);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
@@ -166,6 +201,9 @@ struct rt_camera {
         S.lights = reinterpret_cast<const RtLight*>(b + off_lights);
         S.glights = S.lights;
         S.nodes = reinterpret_cast<const RtNode*>(b + off_nodes);
+        S.onbs = reinterpret_cast<const RtOnb*>(b + off_onbs);
+        S.n_onb = n_onb;
+        S.off_onbs = off_onbs;
         S.blob = d_blob;
         S.lds_words = lds_words;
         S.off_prims = off_prims;

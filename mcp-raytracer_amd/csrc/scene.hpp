@@ -85,6 +85,15 @@ struct alignas(16) RtLight {
 };
 static_assert(sizeof(RtLight) == 16, "RtLight must be 16 bytes");
 
+// Orthonormal basis (ONBasis, src/geometry/onbasis.ts:18-51) of a planar
+// primitive's hit normal, precomputed per face (0: front = the plane normal,
+// 1: back = its negation) and per precision (0: ref, 1: fp32): a diffuse bounce
+// on a quad or plane reads it instead of rebuilding it (two normalisations).
+struct alignas(16) RtOnb {
+    float u[4], v[4], w[4];
+};
+static_assert(sizeof(RtOnb) == 48, "RtOnb must be 48 bytes");
+
 struct RtCamera {
     float pixel00[4];
     float du[4];
