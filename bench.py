@@ -177,6 +177,21 @@ def main():
         except Exception:
             traffic = None
 
+    # VALU evidence of the same kernel (committed rocprofv3 --pmc passes, tools/pmc_valu.sh):
+    # the path is VALU-issue / divergence bound, not HBM bound.
+    valu = None
+    vf = ROOT / "profiles" / "pmc_valu.json"
+    if vf.exists():
+        try:
+            key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n{world}"
+            e = json.loads(vf.read_text()).get(key)
+            if e:
+                valu = {k: e[k] for k in ("kernel", "valu_busy", "lane_util", "clock_ghz", "valu_insts_per_sample",
+                                          "f64_tflops", "f64_peak_tflops", "f64_frac", "duration_ms")}
+                valu["source"] = "profiles/pmc_valu.json"
+        except Exception:
+            valu = None
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
@@ -203,6 +218,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "work_per_sample": {k: round(v / max(counters["samples"], 1), 3)
                                              for k, v in counters.items()}},
+            "valu": valu,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
