@@ -286,11 +286,19 @@ struct rt_camera {
         SampleBuf sb{};
         sb.rec = d_sbuf;
         sb.pool = kWave * env_int("RT_AMD_POOL", 1);
-        // guided schedule: half of the remaining samples per phase, chunks halving
+        // guided schedule: half of the remaining samples per phase, chunks halving.
+        // First-phase chunk from the samples per resident lane: an item is the
+        // critical path of its pixel, so small per-launch workloads (a rank's
+        // share of the image, small images) or a few very expensive pixels (rays
+        // grazing a field of spheres) need short items, while large ones amortise
+        // the hand-out over long items (tools/tail_probe.py sweep).
         {
-            int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", 16), std::max(1, C.n_samples / 2)), np = 0;
+            const double spl = (double)mine * kWave * (double)C.n_samples / ((double)cus * kBlockChunk);
+            int c_auto = 1;
+            while (c_auto * 2 <= 32 && c_auto * 2 * 16 <= spl) c_auto *= 2;  // pow2 floor of spl / 16, in [1, 32]
+            int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2)), np = 0;
             if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
-                c = std::min(env_int("RT_AMD_CHUNK", 16), C.n_samples);
+                c = std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples);
                 const int full = C.n_samples / c;
                 sb.s0[np] = 0; sb.chunk[np] = c; sb.nch[np] = full; ++np;
                 s0 = full * c;
