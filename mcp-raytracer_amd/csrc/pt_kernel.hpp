@@ -217,6 +217,19 @@ __device__ __forceinline__ RayK<Real> make_ray(V3 o, V3 d) {
     return r;
 }
 
+// The ray as the exact (Real) tests inside a traversal loop see it: o and d
+// pass through an empty asm so their conversions to Real (and |d|^2) are
+// redone per test instead of being hoisted out of the loop as long-lived fp64
+// values - which the register allocator then spills to scratch every trip.
+// Values are unchanged; the tests run on a small fraction of loop iterations.
+template <class Real>
+__device__ __forceinline__ RayK<Real> ray_at_use(const RayK<Real>& r) {
+    RayK<Real> q = r;
+    asm volatile("" : "+v"(q.o.x), "+v"(q.o.y), "+v"(q.o.z), "+v"(q.d.x), "+v"(q.d.y), "+v"(q.d.z));
+    q.a = len2<Real>(q.d);
+    return q;
+}
+
 // AABB.hit (src/geometry/aabb.ts:30-55): each axis is clipped against the
 // ORIGINAL interval (the reference does not carry tMin/tMax across axes);
 // comparisons keep the reference's NaN behaviour.
@@ -661,10 +674,10 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
             if (!sphere_maybe(g, f, thi, lo)) continue;
             if (COUNT) count_exact(cnt);
             k = S.tprims[m];
-            cand = sphere_t<Real>(S.prims[k], r, K<Real>::TMIN, (Real)__builtin_inf(), t);
+            cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
         } else {
             k = S.tprims[m];
-            cand = prim_candidate<Real, COUNT>(S.prims[k], r, f, thi, t, cnt);
+            cand = prim_candidate<Real, COUNT>(S.prims[k], ray_at_use<Real>(r), f, thi, t, cnt);
         }
         if (cand && (t < best_t || (t == best_t && k < best))) {
             best_t = t;
@@ -851,7 +864,7 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
         mask &= ~(1u << kb);
         if (COUNT) count_exact(cnt);
         Real t;
-        if (prim_exact<Real>(S.prims[kb], r, t) && (t < best_t || (t == best_t && kb < best))) {
+        if (prim_exact<Real>(S.prims[kb], ray_at_use<Real>(r), t) && (t < best_t || (t == best_t && kb < best))) {
             best_t = t;
             best = kb;
             thi = upper_f<Real>(t);
