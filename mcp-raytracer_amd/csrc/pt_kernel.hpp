@@ -125,6 +125,7 @@ constexpr int kStackStride = 1024;  // LDS traversal-stack column stride (>= any
 #define RT_STACK_TNEAR 0
 #endif
 constexpr bool kStackTnear = RT_STACK_TNEAR != 0;
+static_assert(!(RT_BVH4 && RT_STACK_TNEAR), "the 4-wide traversal keeps 4-byte stack entries");
 constexpr int kTile = 8;          // 8x8 pixels per wave-tile
 constexpr int kEmitStack = 128;   // emission terms kept for the right fold (EMIT builds)
 
@@ -709,6 +710,59 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
         }
         return kTravDone;
     };
+#if RT_BVH4
+    // one 4-wide node step: the nearest hit child is next, the other hit
+    // children are pushed farthest first (so the nearer pop first)
+    auto node_step = [&](int ref) -> int {
+        const RtT4Node* nd = reinterpret_cast<const RtT4Node*>(S.tnodes) + ref;
+        const float4 mnx = *reinterpret_cast<const float4*>(nd->bmin[0]);
+        const float4 mny = *reinterpret_cast<const float4*>(nd->bmin[1]);
+        const float4 mnz = *reinterpret_cast<const float4*>(nd->bmin[2]);
+        const float4 mxx = *reinterpret_cast<const float4*>(nd->bmax[0]);
+        const float4 mxy = *reinterpret_cast<const float4*>(nd->bmax[1]);
+        const float4 mxz = *reinterpret_cast<const float4*>(nd->bmax[2]);
+        const int4 rf = *reinterpret_cast<const int4*>(nd->ref);
+        if (COUNT) cnt[CT_NODE] += 4;
+        const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w}, {mnz.x, mnz.y, mnz.z, mnz.w}};
+        const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
+        const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
+        float key[4];
+        int kr[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float tn = kTminLo, tf = thi;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float t0 = (bmn[a][c] - f.o[a]) * f.inv[a];
+                const float t1 = (bmx[a][c] - f.o[a]) * f.inv[a];
+                tn = ::fmaxf(tn, ::fminf(t0, t1));
+                tf = ::fminf(tf, ::fmaxf(t0, t1));
+            }
+            const bool hit = cr[c] != kT4Empty && tn <= tf * 1.000002f;
+            key[c] = hit ? tn : __builtin_inff();
+            kr[c] = hit ? cr[c] : kTravDone;
+        }
+        // sort (key, ref) ascending: 5 compare-exchanges
+        auto cx = [&](int i, int j) {
+            const bool sw = key[j] < key[i];
+            const float tk = sw ? key[j] : key[i];
+            key[j] = sw ? key[i] : key[j];
+            key[i] = tk;
+            const int tr = sw ? kr[j] : kr[i];
+            kr[j] = sw ? kr[i] : kr[j];
+            kr[i] = tr;
+        };
+        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+#pragma unroll
+        for (int c = 3; c >= 1; --c) {
+            if (kr[c] != kTravDone) {
+                stk[sp * kStackStride] = kr[c];
+                ++sp;
+            }
+        }
+        return kr[0] != kTravDone ? kr[0] : pop();
+    };
+#else
     // one node step: the next node / leaf to visit
     auto node_step = [&](int ref) -> int {
         const RtTNode nd = S.tnodes[ref];
@@ -726,6 +780,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
         if (ha || hb) return ha ? nd.box[0].a : nd.box[1].a;
         return pop();
     };
+#endif
     int ref = S.troot;
 #if RT_TRAV_WW
     int leaf = kTravDone;  // parked leaf

@@ -148,7 +148,8 @@ struct rt_camera {
         if (device == dev) return;
         if (device >= 0) release();
         std::vector<char> blob;
-        append(blob, build.tnodes, nullptr);
+        if (RT_BVH4) append(blob, build.t4nodes, nullptr);  // the fast traversal's tree heads the blob
+        else append(blob, build.tnodes, nullptr);
         append(blob, build.tprims, &off_tprims);
         append(blob, build.tsph, &off_tsph);
         append(blob, build.prims, &off_prims);
@@ -210,7 +211,7 @@ struct rt_camera {
         S.off_mats = off_mats;
         S.off_lights = off_lights;
         S.lds_stack_bytes = 0;
-        S.troot = build.troot;
+        S.troot = RT_BVH4 ? build.t4root : build.troot;
         S.root_box = build.troot_box;
         S.cam = build.cam;
         S.mix_total = mix_total;

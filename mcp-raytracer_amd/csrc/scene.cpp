@@ -929,6 +929,66 @@ std::vector<RtTNode> make_tnodes(const std::vector<RtNode>& f, int32_t& root_ref
     return out;
 }
 
+// The padded binary tree (DFS, node 0 = root) collapsed to 4-wide nodes: each
+// 4-node takes a binary node's two children and keeps replacing its largest
+// interior child by that child's two children until it holds four. Boxes are
+// the binary tree's (padded) boxes, so every primitive stays inside each box on
+// its path; boxes the reference can never enter (NaN-marked) become empty slots.
+static int32_t t4_leaf_ref(const RtNode& n) {
+    const int32_t count = -n.b;
+    if (count < 1 || count > 7 || n.a >= (1 << 27)) throw std::runtime_error("BVH leaf does not fit the TNode code");
+    return ~((n.a << 3) | count);
+}
+static double t4_area(const RtNode& n) {
+    double e[3];
+    for (int a = 0; a < 3; ++a) {
+        e[a] = (double)n.bmax[a] - (double)n.bmin[a];
+        if (!(e[a] >= 0) || !std::isfinite(e[a])) e[a] = 1e30;
+    }
+    return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
+}
+static int32_t t4_build(const std::vector<RtNode>& f, int32_t i, int depth, std::vector<RtT4Node>& out, int& max_depth) {
+    max_depth = std::max(max_depth, depth);
+    std::vector<int32_t> ch = {f[(size_t)i].a, f[(size_t)i].b};
+    while (ch.size() < 4) {
+        int best = -1;
+        double best_a = -1.0;
+        for (size_t k = 0; k < ch.size(); ++k) {
+            const RtNode& c = f[(size_t)ch[k]];
+            if (c.b >= 0 && !std::isnan(c.bmin[0]) && t4_area(c) > best_a) { best_a = t4_area(c); best = (int)k; }
+        }
+        if (best < 0) break;
+        const RtNode c = f[(size_t)ch[(size_t)best]];
+        ch[(size_t)best] = c.a;
+        ch.insert(ch.begin() + best + 1, c.b);
+    }
+    const int32_t idx = (int32_t)out.size();
+    out.push_back(RtT4Node{});
+    for (int k = 0; k < 4; ++k) {
+        RtT4Node& t = out[(size_t)idx];
+        for (int a = 0; a < 3; ++a) { t.bmin[a][k] = NAN; t.bmax[a][k] = NAN; }
+        t.ref[k] = kT4Empty;
+        t.pad[k] = 0;
+    }
+    for (size_t k = 0; k < ch.size(); ++k) {
+        const RtNode& c = f[(size_t)ch[k]];
+        if (std::isnan(c.bmin[0])) continue;  // the reference never enters it: no hit below
+        const int32_t r = c.b >= 0 ? t4_build(f, ch[k], depth + 1, out, max_depth) : t4_leaf_ref(c);
+        RtT4Node& t = out[(size_t)idx];
+        for (int a = 0; a < 3; ++a) { t.bmin[a][k] = c.bmin[a]; t.bmax[a][k] = c.bmax[a]; }
+        t.ref[k] = r;
+    }
+    return idx;
+}
+std::vector<RtT4Node> make_t4nodes(const std::vector<RtNode>& f, int32_t& root_ref, int& depth) {
+    std::vector<RtT4Node> out;
+    depth = 0;
+    if (f.empty()) { root_ref = ~0; return out; }
+    if (f[0].b < 0) { root_ref = t4_leaf_ref(f[0]); return out; }
+    root_ref = t4_build(f, 0, 1, out, depth);
+    return out;
+}
+
 // ---------------------------------------------------------------------------
 // Fast-traversal tree built for speed, not for the reference's visiting order:
 // the fast traversal returns the (t, slot) minimum over all primitives, so any
@@ -1251,12 +1311,14 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
             b.out.tprims = sb.order;
             const std::vector<RtNode> padded = make_fast_nodes(sb.nodes);
             b.out.tnodes = make_tnodes(padded, b.out.troot);
+            b.out.t4nodes = make_t4nodes(padded, b.out.t4root, b.out.t4depth);
             b.out.troot_box = padded[0];
             b.out.tdepth = sb.depth_seen;
         } else {
             b.out.tprims.resize(b.out.prims.size());
             for (size_t k = 0; k < b.out.tprims.size(); ++k) b.out.tprims[k] = (int32_t)k;
             b.out.tnodes = make_tnodes(b.out.fnodes, b.out.troot);
+            b.out.t4nodes = make_t4nodes(b.out.fnodes, b.out.t4root, b.out.t4depth);
             b.out.troot_box = b.out.fnodes[0];
             b.out.tdepth = b.out.bvh_depth;
         }
@@ -1270,7 +1332,9 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
                 for (int c = 0; c < 4; ++c) b.out.tsph[m * 4 + c] = p.g0[c];
         }
     }
-    cam.stack_depth = std::max(b.out.bvh_depth, b.out.tdepth) + 1;
+    // stack entries: reference DFS (depth + 1), binary fast tree (depth + 1),
+    // 4-wide tree (up to 3 pushes per level + 1)
+    cam.stack_depth = std::max(b.out.bvh_depth, RT_BVH4 ? 3 * b.out.t4depth + 1 : b.out.tdepth) + 1;
     b.out.fast_ok = prims_inside_boxes(b.out.prims);
     return std::move(b.out);
 }

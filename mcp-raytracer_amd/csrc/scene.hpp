@@ -54,6 +54,23 @@ struct alignas(16) RtTNode {
 };
 static_assert(sizeof(RtTNode) == 64, "RtTNode must be 64 bytes");
 
+// Fast traversal over 4-wide nodes (1) or the binary children-in-parent tree (0).
+#ifndef RT_BVH4
+#define RT_BVH4 1
+#endif
+
+// 4-wide fast-traversal node (RT_BVH4): four children's boxes as [axis][child]
+// rows (one ds_read_b128 per row) and their references (node index, leaf code
+// as in RtTNode, or kTravDone for an empty slot).
+struct alignas(16) RtT4Node {
+    float bmin[3][4];
+    float bmax[3][4];
+    int32_t ref[4];
+    int32_t pad[4];
+};
+static_assert(sizeof(RtT4Node) == 128, "RtT4Node must be 128 bytes");
+constexpr int32_t kT4Empty = (int32_t)0x80000000;  // empty child slot (= kTravDone)
+
 struct alignas(16) RtPrim {
     int32_t type;
     int32_t mat;
@@ -142,6 +159,9 @@ struct SceneBuild {
     std::vector<RtTNode> tnodes; // fast-traversal tree, children-in-parent (SAH, or the reference tree)
     std::vector<int32_t> tprims; // its leaves' primitive slots (padded to a multiple of 4)
     std::vector<float> tsph;     // per tprims entry: sphere {centre, fp32 radius}, NaNs for other types
+    std::vector<RtT4Node> t4nodes; // the same tree collapsed to 4-wide nodes (RT_BVH4)
+    int32_t t4root = 0;          // its root reference
+    int t4depth = 0;             // its depth in 4-wide nodes
     int32_t troot = 0;           // reference of the root (TNode index or leaf code)
     int tdepth = 0;              // its depth (root = 1)
     RtNode troot_box{};          // its root box (padded)
