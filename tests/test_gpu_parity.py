@@ -441,3 +441,93 @@ def test_full_size_headline_partition_and_determinism(rt, gpu):
         acc_rad += prad
     assert total == W * H
     assert torch.equal(acc, full) and torch.equal(acc_rad, rad)
+
+
+def _random_scene(seed):
+    """A randomized custom SceneData: 1-40 objects (brute force up to 16, the 4-wide tree above),
+    every material kind (nested mixed/layered, emissive), axis-aligned and tilted quads, planes,
+    quad and sphere lights, sometimes a negative-radius sphere (reference-order traversal) and
+    a lens aperture."""
+    r = np.random.default_rng(seed)
+
+    def col():
+        return [round(float(x), 3) for x in r.uniform(0.05, 0.95, 3)]
+
+    def base_mat():
+        k = r.integers(0, 4)
+        if k == 0:
+            return {"type": "lambert", "color": col()}
+        if k == 1:
+            return {"type": "metal", "color": col(), "fuzz": round(float(r.uniform(0, 0.6)), 3)}
+        if k == 2:
+            return {"type": "glass", "ior": round(float(r.uniform(1.2, 2.0)), 3)}
+        return {"type": "light", "emit": [round(float(x), 2) for x in r.uniform(0.5, 6, 3)]}
+
+    mats = [{"id": f"m{i}", "material": base_mat()} for i in range(5)]
+    mats.append({"id": "mx", "material": {"type": "mixed", "diff": "m0", "spec": base_mat(),
+                                          "weight": round(float(r.uniform(0.1, 0.9)), 3)}})
+    mats.append({"id": "ly", "material": {"type": "layered", "outer": {"type": "glass", "ior": 1.5},
+                                          "inner": base_mat()}})
+    ids = [m["id"] for m in mats]
+    objs = []
+    n = int(r.integers(1, 41))
+    for _ in range(n):
+        k = r.integers(0, 10)
+        pos = [round(float(x), 3) for x in r.uniform(-2, 2, 3)]
+        mat = ids[int(r.integers(0, len(ids)))]
+        if k < 6:
+            rad = round(float(r.uniform(0.1, 0.7)), 3)
+            if r.random() < 0.05:
+                rad = -rad
+            objs.append({"type": "sphere", "pos": pos, "r": rad, "material": mat})
+        elif k < 9:
+            if r.random() < 0.5:  # axis-aligned
+                a = int(r.integers(0, 3))
+                u = [0.0, 0.0, 0.0]
+                v = [0.0, 0.0, 0.0]
+                u[(a + 1) % 3] = round(float(r.uniform(0.3, 2)), 3)
+                v[(a + 2) % 3] = round(float(r.uniform(0.3, 2)), 3)
+            else:
+                u = [round(float(x), 3) for x in r.uniform(-1.5, 1.5, 3)]
+                v = [round(float(x), 3) for x in r.uniform(-1.5, 1.5, 3)]
+            objs.append({"type": "quad", "pos": pos, "u": u, "v": v, "material": mat})
+        else:
+            objs.append({"type": "plane", "pos": [0, -2.5, 0], "u": [1, 0, 0], "v": [0, 0, -1], "material": mat})
+        if r.random() < 0.15 and objs[-1]["type"] != "plane":
+            objs[-1]["light"] = True
+    ap = 0.05 if r.random() < 0.3 else 0.0
+    return {"camera": {"vfov": 45, "from": [0.3, 1.0, 6.0], "at": [0, 0, 0], "up": [0, 1, 0], "aperture": ap,
+                       "focus": 6.0 if ap else 0,
+                       "background": {"type": "gradient", "top": [0.5, 0.7, 1.0], "bottom": [1, 1, 1]}},
+            "materials": mats, "objects": objs}
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_scenes_match_oracle(rt, oracle, gpu, seed):
+    sd = _random_scene(seed)
+    ro = {"width": 32, "samples": 4, "depth": 8, **NOADAPT}
+    orc = oracle.render(sd, ro)
+    for trav in ("auto", "fast", "brute", "reference"):
+        cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
+        rgb_eq, rad_eq, maxd = _agreement(rad, rgb, orc["radiance"], orc["rgb"])
+        assert rgb_eq >= 0.995 and rad_eq >= 0.995, (seed, trav, len(sd["objects"]), rgb_eq, rad_eq, maxd)
+        assert st.samples["total"] == orc["stats"]["samples"]["total"]
+
+
+def test_edge_cases_match_oracle(rt, oracle, gpu):
+    """No objects (the reference's BVHNode dereferences a null box: the same error),
+    a single-pixel-wide image, samples = 1 (no jitter)."""
+    empty = {"camera": {"vfov": 40, "from": [0, 0, 3], "at": [0, 0, 0], "up": [0, 1, 0],
+                        "background": {"type": "gradient", "top": [0.2, 0.4, 1.0], "bottom": [1, 0.9, 0.8]}},
+             "materials": [], "objects": []}
+    with pytest.raises(rt.RtError, match="reading 'maximum'"):
+        rt.create_camera_from_scene_data(empty, {"width": 16})
+    for sd, ro in [(rt.generate_scene_data({"type": "cornell"}), {"width": 1, "aspect": 0.25, "samples": 8, "depth": 8}),
+                   (rt.generate_scene_data({"type": "cornell"}), {"width": 24, "samples": 1, "depth": 8})]:
+        ro = {**ro, **NOADAPT}
+        orc = oracle.render(sd, ro)
+        cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+        assert rgb.shape == orc["rgb"].shape
+        rgb_eq, rad_eq, maxd = _agreement(rad, rgb, orc["radiance"], orc["rgb"])
+        assert rgb_eq == 1.0 and rad_eq == 1.0, (ro, maxd)
+        assert st.pixels == orc["stats"]["pixels"] and st.samples["total"] == orc["stats"]["samples"]["total"]
