@@ -820,6 +820,164 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     return best;
 }
 
+// ---------------------------------------------------------------------------
+// Resumable fast traversal (chunked kernel, RT_RESUME). closest_hit_fast keeps
+// the whole wave in its loop until the lane with the longest walk is done - a
+// ray grazing a field of spheres can need ten times the mean node visits, and
+// every other lane idles meanwhile. Here a lane's walk state persists across
+// the wave's loop iterations: the wave walks until `min_ready` of its lanes are
+// done, they shade and start their next rays, and the long walks continue next
+// to them. Same walk (culling, parked leaves, (t, slot) minimum) as
+// closest_hit_fast, so the same hit.
+// ---------------------------------------------------------------------------
+#ifndef RT_RESUME
+#define RT_RESUME 1
+#endif
+template <class Real>
+struct FastWalk {
+    int ref, leaf, sp, best;
+    float thi;
+    Real best_t;
+};
+
+template <class Real, bool COUNT>
+__device__ __forceinline__ void fast_walk_begin(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, uint32_t* cnt) {
+    const FRay f = make_fray(o, d);
+    W.best_t = (Real)__builtin_inf();
+    W.best = -1;
+    W.thi = __builtin_inff();
+    W.sp = 0;
+    W.leaf = kTravDone;
+    float tn0;
+    if (COUNT) cnt[CT_NODE]++;
+    W.ref = slab(S.root_box, f, W.thi, tn0) ? S.troot : kTravDone;
+}
+
+// Called by the whole wave with uniform control flow; lanes with `walking`
+// advance their walks. Returns when no lane walks, or (unless `drain`) after at
+// least one round once `min_ready` lanes of the wave are not walking.
+template <class Real, bool COUNT>
+__device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, bool& walking,
+                                                 int* stk, int min_ready, bool drain, uint32_t* cnt) {
+    const FRay f = make_fray(o, d);
+    const RayK<Real> r = make_ray<Real>(o, d);
+    float* stkt = nullptr;
+    (void)stkt;
+    int rounds = 0;
+    while (true) {
+        const unsigned long long wm = __ballot(walking);
+        if (wm == 0ull) break;
+        if (rounds > 0 && !drain && kWave - __popcll(wm) >= min_ready) break;
+        ++rounds;
+        if (walking) {
+            int sp = W.sp;
+            float thi = W.thi;
+            auto pop = [&]() -> int {
+                if (sp > 0) {
+                    --sp;
+                    return stk[sp * kStackStride];
+                }
+                return kTravDone;
+            };
+#if RT_BVH4
+            auto node_step = [&](int ref) -> int {
+                const RtT4Node* nd = reinterpret_cast<const RtT4Node*>(S.tnodes) + ref;
+                const float4 mnx = *reinterpret_cast<const float4*>(nd->bmin[0]);
+                const float4 mny = *reinterpret_cast<const float4*>(nd->bmin[1]);
+                const float4 mnz = *reinterpret_cast<const float4*>(nd->bmin[2]);
+                const float4 mxx = *reinterpret_cast<const float4*>(nd->bmax[0]);
+                const float4 mxy = *reinterpret_cast<const float4*>(nd->bmax[1]);
+                const float4 mxz = *reinterpret_cast<const float4*>(nd->bmax[2]);
+                const int4 rf = *reinterpret_cast<const int4*>(nd->ref);
+                if (COUNT) cnt[CT_NODE] += 4;
+                const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w},
+                                         {mnz.x, mnz.y, mnz.z, mnz.w}};
+                const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w},
+                                         {mxz.x, mxz.y, mxz.z, mxz.w}};
+                const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
+                float key[4];
+                int kr[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    float tn = kTminLo, tf = thi;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        const float t0 = (bmn[a][c] - f.o[a]) * f.inv[a];
+                        const float t1 = (bmx[a][c] - f.o[a]) * f.inv[a];
+                        tn = ::fmaxf(tn, ::fminf(t0, t1));
+                        tf = ::fminf(tf, ::fmaxf(t0, t1));
+                    }
+                    const bool hit = cr[c] != kT4Empty && tn <= tf * 1.000002f;
+                    key[c] = hit ? tn : __builtin_inff();
+                    kr[c] = hit ? cr[c] : kTravDone;
+                }
+                auto cx = [&](int i, int j) {
+                    const bool sw = key[j] < key[i];
+                    const float tk = sw ? key[j] : key[i];
+                    key[j] = sw ? key[i] : key[j];
+                    key[i] = tk;
+                    const int tr = sw ? kr[j] : kr[i];
+                    kr[j] = sw ? kr[i] : kr[j];
+                    kr[i] = tr;
+                };
+                cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+#pragma unroll
+                for (int c = 3; c >= 1; --c) {
+                    if (kr[c] != kTravDone) {
+                        stk[sp * kStackStride] = kr[c];
+                        ++sp;
+                    }
+                }
+                return kr[0] != kTravDone ? kr[0] : pop();
+            };
+#else
+            auto node_step = [&](int ref) -> int {
+                const RtTNode nd = S.tnodes[ref];
+                float ta, tb;
+                if (COUNT) cnt[CT_NODE] += 2;
+                const bool ha = slab(nd.box[0], f, thi, ta);
+                const bool hb = slab(nd.box[1], f, thi, tb);
+                if (ha && hb) {
+                    const bool a_first = ta <= tb;
+                    stk[sp * kStackStride] = a_first ? nd.box[1].a : nd.box[0].a;
+                    ++sp;
+                    return a_first ? nd.box[0].a : nd.box[1].a;
+                }
+                if (ha || hb) return ha ? nd.box[0].a : nd.box[1].a;
+                return pop();
+            };
+#endif
+            // one round of closest_hit_fast's parked-leaf walk
+            int ref = W.ref, leaf = W.leaf;
+            while (ref >= 0) {
+                ref = node_step(ref);
+                if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
+                    leaf = ref;
+                    ref = pop();
+                }
+                if (__ballot(leaf == kTravDone) == 0ull) break;  // every walking lane holds a leaf
+            }
+            if (leaf == kTravDone && ref != kTravDone) {
+                leaf = ref;
+                ref = pop();
+            }
+            while (leaf != kTravDone) {
+                leaf_test<Real, COUNT>(S, leaf, r, f, thi, W.best_t, W.best, cnt);
+                leaf = kTravDone;
+                if (ref < 0 && ref != kTravDone) {
+                    leaf = ref;
+                    ref = pop();
+                }
+            }
+            W.ref = ref;
+            W.leaf = leaf;
+            W.sp = sp;
+            W.thi = thi;
+            if (ref == kTravDone && leaf == kTravDone) walking = false;
+        }
+    }
+}
+
 // Small scenes: test every primitive in leaf order. The answer is the same
 // lexicographic minimum of (t, leaf slot) the fast traversal returns (valid
 // under the same condition, SceneBuild::fast_ok). The loop bound and the
@@ -1224,27 +1382,44 @@ __device__ __forceinline__ void path_begin(const RtCamera& C, Path<EMIT>& P, V3 
 // One level of rayColor (src/camera.ts:221-319). Returns true when the path
 // ends; `c` is then the sample's radiance (the recursion's emitted + ... right
 // fold included).
-template <class Real, bool EMIT, bool COUNT, bool PROF, int TRAV>
-__device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, Path<EMIT>& P, int* stk, float* stkt,
-                                          uint32_t* cnt, unsigned long long& st_err, Prof& pf, V3& c) {
+// The emission right fold of a terminated path (EMIT builds).
+template <bool EMIT>
+__device__ __forceinline__ void fold_emission(const Path<EMIT>& P, V3& c) {
+    if (EMIT) {
+        for (int k = min(P.em_n, kEmitStack) - 1; k >= 0; --k) c = add(P.em[k], c);
+    }
+}
+
+// First half of a rayColor level: the depth cut-off and Russian roulette
+// (src/camera.ts:221-235). Returns true when the path ends here (`c` is then
+// the sample's radiance), false when its ray must be traced next.
+template <class Real, bool EMIT, bool PROF>
+__device__ __forceinline__ bool path_pre(const RtCamera& C, Path<EMIT>& P, Prof& pf, V3& c) {
     bool term = false;
     c = v3(0, 0, 0);
     if (P.bounces >= C.depth) {
         term = true;
-    } else {
-        if (C.roulette && P.bounces >= C.roulette_depth) {
-            const Real mc = js_max<Real>(js_max<Real>((Real)P.T.x, (Real)P.T.y), (Real)P.T.z);
-            const Real p = js_min<Real>(mc, (Real)0.95);
-            if (uniform<Real>(P.rng) > p) term = true;
-            else P.T = divs<Real>(P.T, p);
-        }
-        if (!term) {
-            const RayK<Real> ray = make_ray<Real>(P.o, P.d);
-            Real t;
-            if (COUNT) cnt[CT_RAYS]++;
-            psec<PROF>(pf, PR_RR);
-            const int h = closest_hit_any<Real, COUNT, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
-            psec<PROF>(pf, PR_HIT);
+    } else if (C.roulette && P.bounces >= C.roulette_depth) {
+        const Real mc = js_max<Real>(js_max<Real>((Real)P.T.x, (Real)P.T.y), (Real)P.T.z);
+        const Real p = js_min<Real>(mc, (Real)0.95);
+        if (uniform<Real>(P.rng) > p) term = true;
+        else P.T = divs<Real>(P.T, p);
+    }
+    if (term) fold_emission<EMIT>(P, c);
+    psec<PROF>(pf, PR_RR);
+    return term;
+}
+
+// Second half: given the closest hit (h, t) of the path's ray, the miss /
+// emission / scatter / light sampling of the same level (src/camera.ts:236-319).
+// Returns true when the path ends (`c` = the sample's radiance).
+template <class Real, bool EMIT, bool COUNT, bool PROF>
+__device__ __forceinline__ bool path_post(const DevScene& S, const RtCamera& C, Path<EMIT>& P, int h, Real t,
+                                          uint32_t* cnt, unsigned long long& st_err, Prof& pf, V3& c) {
+    bool term = false;
+    c = v3(0, 0, 0);
+    {
+        {
             if (h < 0) {
                 term = true;
                 if (!C.has_background) st_err |= ERR_NO_BACKGROUND;
@@ -1341,10 +1516,23 @@ __device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, 
         }
     }
     // emitted.add(rayColor(...)) at every level: a right fold.
-    if (EMIT && term) {
-        for (int k = min(P.em_n, kEmitStack) - 1; k >= 0; --k) c = add(P.em[k], c);
-    }
+    if (term) fold_emission<EMIT>(P, c);
     return term;
+}
+
+// One level of rayColor (src/camera.ts:221-319): path_pre, the closest hit,
+// path_post. Returns true when the path ends; `c` is then the sample's radiance
+// (the recursion's emitted + ... right fold included).
+template <class Real, bool EMIT, bool COUNT, bool PROF, int TRAV>
+__device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, Path<EMIT>& P, int* stk, float* stkt,
+                                          uint32_t* cnt, unsigned long long& st_err, Prof& pf, V3& c) {
+    if (path_pre<Real, EMIT, PROF>(C, P, pf, c)) return true;
+    const RayK<Real> ray = make_ray<Real>(P.o, P.d);
+    Real t;
+    if (COUNT) cnt[CT_RAYS]++;
+    const int h = closest_hit_any<Real, COUNT, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
+    psec<PROF>(pf, PR_HIT);
+    return path_post<Real, EMIT, COUNT, PROF>(S, C, P, h, t, cnt, st_err, pf, c);
 }
 
 // Per-pixel result: finalColor (src/camera.ts:326-340) + writeColorToBuffer
@@ -1568,6 +1756,7 @@ struct SampleBuf {
     int32_t n_phases;
     int32_t n_items;
     int32_t refill_min;  // idle lanes that trigger a hand-out (all-idle always does)
+    int32_t min_ready;   // resumable fast traversal: lanes done walking before the wave shades
     int32_t s0[kMaxPhases], chunk[kMaxPhases], nch[kMaxPhases], item_base[kMaxPhases];
     double rnch[kMaxPhases];  // 1.0 / nch
 };
@@ -1633,6 +1822,10 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     bool new_path = false;
     Path<EMIT> P;
     const double rtx = 1.0 / (double)tiles_x;
+    // resumable fast traversal (product builds): per-lane walk state across iterations
+    constexpr bool RS = RT_RESUME && TRAV == TRAV_FAST && INSTR == 0;
+    FastWalk<Real> W;
+    bool walking = false;
 
     while (true) {
         // hand out items to idle lanes (wave-uniform control flow); waits until
@@ -1680,7 +1873,43 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             if (exhausted) break;
             continue;
         }
-        if (slot >= 0) {
+        if constexpr (RS) {
+            // the sample's radiance and bounce count to its record; next sample or idle
+            auto finish_sample = [&](V3 c) {
+                float4 r;
+                r.x = c.x;
+                r.y = c.y;
+                r.z = c.z;
+                r.w = __int_as_float(P.bounces);
+                sb.rec[(size_t)s * sb.slots + slot] = r;
+                ++s;
+                if (s < s_end) new_path = true;
+                else slot = -1;
+            };
+            const RtCamera& C = cam_opaque();
+            // lanes between rays: start a path if needed, then the level's depth
+            // cut-off / roulette, and the walk of its ray
+            if (slot >= 0 && !walking) {
+                if (new_path) {
+                    path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)s);
+                    new_path = false;
+                }
+                V3 c;
+                if (path_pre<Real, EMIT, PROF>(C, P, pf, c)) {
+                    finish_sample(c);
+                } else {
+                    fast_walk_begin<Real, COUNT>(S, P.o, P.d, W, cnt);
+                    walking = true;
+                }
+            }
+            const bool was_walking = walking;
+            fast_walk_rounds<Real, COUNT>(S, P.o, P.d, W, walking, stk, sb.min_ready, exhausted, cnt);
+            // walks that ended: the rest of the level (miss / emission / scatter / light sampling)
+            if (was_walking && !walking) {
+                V3 c;
+                if (path_post<Real, EMIT, COUNT, PROF>(S, C, P, W.best, W.best_t, cnt, st_err, pf, c)) finish_sample(c);
+            }
+        } else if (slot >= 0) {
             const RtCamera& C = cam_opaque();
             if (PROF) { pf.tl = pf.tt; pf.secs[PR_TRIPS]++; }
             if (new_path) {

@@ -327,6 +327,7 @@ struct rt_camera {
             if (covered != C.n_samples) throw std::runtime_error("guided schedule: coverage");
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
+            sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
         }
         for (long t0 = 0; t0 < mine; t0 += pass_tiles) {
             const long nt = std::min(pass_tiles, mine - t0);
