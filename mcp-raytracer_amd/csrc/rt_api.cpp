@@ -294,9 +294,12 @@ struct rt_camera {
         // grazing a field of spheres) need short items, while large ones amortise
         // the hand-out over long items (tools/tail_probe.py sweep).
         {
+            // BVH scenes have heavy-tailed per-ray cost (grazing rays): spl / 16; brute-force
+            // scenes test every primitive per ray (bounded cost): spl / 8
             const double spl = (double)mine * kWave * (double)C.n_samples / ((double)cus * kBlockChunk);
+            const double per = v.trav == TRAV_BRUTE ? 8.0 : 16.0;
             int c_auto = 1;
-            while (c_auto * 2 <= 32 && c_auto * 2 * 16 <= spl) c_auto *= 2;  // pow2 floor of spl / 16, in [1, 32]
+            while (c_auto * 2 <= 32 && c_auto * 2 * per <= spl) c_auto *= 2;  // pow2 floor of spl / per, in [1, 32]
             int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2)), np = 0;
             if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
                 c = std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples);
