@@ -56,10 +56,36 @@ def cpu_baseline(scene_data, ropts, width, height, spp, target_s=15.0):
     out = pyoracle.render(scene_data, ropts, row_step=step, threads=1)
     dt = time.perf_counter() - t0
     samples = out["stats"]["samples"]["total"]
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+    line = {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
             "sample": f"rows j%{step}==0 of the {width}x{height} image at spp={spp} "
                       f"({int(out['stats']['pixels'])} px, {int(samples)} samples, {dt:.1f} s), "
                       f"oracle/oracle.cpp ref precision, single thread"}
+    # the same restatement over all of this process's host cores
+    # (threads over rows, the analogue of the reference's -p workers), ~target_s/2 of work.
+    # The GPU box grants a 16-CPU share whatever nproc says.
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    if cores > 1:
+        step_mt = max(1, step * 2 // cores)
+        t0 = time.perf_counter()
+        out = pyoracle.render(scene_data, ropts, row_step=step_mt, threads=cores)
+        dt = time.perf_counter() - t0
+        s_mt = out["stats"]["samples"]["total"]
+        line["multi_core"] = {"value": s_mt / dt / 1e6, "unit": "Msamples/s", "cores": cores,
+                              "cpu": _cpu_model(),
+                              "sample": f"rows j%{step_mt}==0 ({int(s_mt)} samples, {dt:.1f} s), "
+                                        f"{cores} threads over rows"}
+    return line
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
