@@ -25,9 +25,17 @@ _COMMON = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-
            f"-I{CSRC}", f"-I{INCLUDE}"]
 
 # (source, extra flags, is_hip)
+# -fno-slp-vectorize on the kernel units: the SLP vectoriser packs pairs of fp32
+# ray/box operations into v_pk_* instructions, which need their operands in
+# register pairs of every pairing used and so keep several copies of the ray
+# live through the traversal loops. Without it the Cornell chunk kernel drops
+# from 128 VGPRs + 8 spilled (scratch reloads inside the pre-filter loop) to
+# 111 VGPRs and no spills: Cornell 7071 -> 7647, spheres-500 4878 -> 5096,
+# rain 19821 -> 20212 Msamples/s (profiles/r01/noslp/).
+_KERNEL_FLAGS = ["-fno-slp-vectorize"]
 _UNITS = [
-    ("pt_ref.hip", ["-ffp-contract=off"], True),
-    ("pt_fp32.hip", ["-ffp-contract=fast"], True),
+    ("pt_ref.hip", ["-ffp-contract=off", *_KERNEL_FLAGS], True),
+    ("pt_fp32.hip", ["-ffp-contract=fast", *_KERNEL_FLAGS], True),
     ("rt_api.cpp", ["-ffp-contract=off", "-x", "hip"], True),
     ("scene.cpp", ["-ffp-contract=off"], False),
 ]
@@ -46,9 +54,10 @@ def _newest_input() -> float:
     return max(p.stat().st_mtime for p in paths)
 
 
-def build_native(force: bool = False, verbose: bool = False, variant: str = "", defines=()) -> Path:
+def build_native(force: bool = False, verbose: bool = False, variant: str = "", defines=(), flags=()) -> Path:
     """Compile (if stale) and return the path of librt_amd.so. `variant` + `defines`
-    build an experimental lib/librt_amd_<variant>.so (loaded with RT_AMD_VARIANT)."""
+    (+ extra compiler `flags`) build an experimental lib/librt_amd_<variant>.so
+    (loaded with RT_AMD_VARIANT)."""
     lib_path = LIB_PATH.with_name(f"librt_amd_{variant}.so") if variant else LIB_PATH
     if not force and lib_path.exists() and lib_path.stat().st_mtime >= _newest_input():
         return lib_path
@@ -57,9 +66,9 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "", 
     obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     objs = []
-    for src, flags, is_hip in _UNITS:
+    for src, uflags, is_hip in _UNITS:
         obj = obj_dir / (src.replace(".", "_") + ".o")
-        cmd = [cc, *_COMMON, *flags, *[f"-D{d}" for d in defines]]
+        cmd = [cc, *_COMMON, *uflags, *flags, *[f"-D{d}" for d in defines]]
         if is_hip:
             cmd.append(f"--offload-arch={ARCH}")
         cmd += ["-c", str(CSRC / src), "-o", str(obj)]

@@ -11,6 +11,7 @@ for v in main $VARIANTS; do
   if [ $v = main ]; then unset RT_AMD_VARIANT; else export RT_AMD_VARIANT=$v; fi
   $B > gpurun_out/ab_cornell_$v.log 2>&1 || exit $?
   $B --scene spheres --spp 64 --depth 8 > gpurun_out/ab_spheres_$v.log 2>&1 || exit $?
+  if [ -n "$FP32" ]; then $B --precision fp32 > gpurun_out/ab_cornellf32_$v.log 2>&1 || exit $?; fi
   if [ -n "$RAIN" ]; then $B --scene rain --width 1920 --spp 128 --depth 16 --steps 3 > gpurun_out/ab_rain_$v.log 2>&1 || exit $?; fi
 done
 exit 0
