@@ -50,6 +50,9 @@ __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long*
     if (t == 0) *tile_counter = 0u;
 }
 
+#ifndef RT_ACC_UNROLL
+#define RT_ACC_UNROLL 8
+#endif
 // Adds every pixel's samples in sample order (PixelStats.add), then
 // finalColor / u8 / RenderStats exactly as the sequential kernel.
 __global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
@@ -66,16 +69,16 @@ __global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg
             unsigned long long bsum = 0;
             int bmin = 0x7fffffff, bmax = 0;
             const int n = C.n_samples;
-            // records are [sample][slot] (coalesced across the wave); 8 loads in flight
+            // records are [sample][slot] (coalesced across the wave); RT_ACC_UNROLL loads in flight
             const float4* rec = sb.rec + slot;
             const size_t stride = (size_t)sb.slots;
             int k = 0;
-            for (; k + 8 <= n; k += 8) {
-                float4 r[8];
+            for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
+                float4 r[RT_ACC_UNROLL];
 #pragma unroll
-                for (int m = 0; m < 8; ++m) r[m] = rec[(size_t)(k + m) * stride];
+                for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = rec[(size_t)(k + m) * stride];
 #pragma unroll
-                for (int m = 0; m < 8; ++m) {
+                for (int m = 0; m < RT_ACC_UNROLL; ++m) {
                     color = add(color, v3(r[m].x, r[m].y, r[m].z));
                     const int b = __float_as_int(r[m].w);
                     bsum += (unsigned long long)b;
