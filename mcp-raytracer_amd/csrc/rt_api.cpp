@@ -286,7 +286,7 @@ struct rt_camera {
         ensure_sbuf((size_t)pass_tiles * rec_per_tile);
         SampleBuf sb{};
         sb.rec = d_sbuf;
-        sb.pool = kWave * env_int("RT_AMD_POOL", 1);
+
         // guided schedule: half of the remaining samples per phase, chunks halving.
         // First-phase chunk from the samples per resident lane: an item is the
         // critical path of its pixel, so small per-launch workloads (a rank's
@@ -297,6 +297,11 @@ struct rt_camera {
             // BVH scenes have heavy-tailed per-ray cost (grazing rays): spl / 16; brute-force
             // scenes test every primitive per ray (bounded cost): spl / 8
             const double spl = (double)mine * kWave * (double)C.n_samples / ((double)cus * kBlockChunk);
+            // items a wave takes per global atomic: two tile-chunks for large brute-force
+            // launches (bounded per-ray cost: fewer atomics, Cornell 800^2 spp256 +2 %),
+            // one otherwise (BVH scenes' heavy-tailed rays: wider takes cost spheres-500
+            // 6-16 %; a rank's 1/2 share of Cornell: -9 %, 1/8: -4 %; profiles/r01/sweep_b/)
+            sb.pool = kWave * env_int("RT_AMD_POOL", v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             const double per = v.trav == TRAV_BRUTE ? 8.0 : 16.0;
             int c_auto = 1;
             while (c_auto * 2 <= 32 && c_auto * 2 * per <= spl) c_auto *= 2;  // pow2 floor of spl / per, in [1, 32]
