@@ -3,15 +3,21 @@
 headline config (Cornell 800x800, spp=256, depth=16), 1..N GPUs.
 
 One step = one full-image render (every pixel x spp paths) with the scene and
-camera already resident in HBM, plus - for N > 1 - the RCCL reduce that
-assembles the tile-interleaved framebuffer on rank 0. Rank 0 prints one JSON
-line. Launch N > 1 with torch.distributed.run (one process per GPU).
+camera already resident in HBM, plus - for N > 1 - the RCCL gather of every
+rank's tile-packed slab to rank 0 and its unpack into the frame. Rank 0 prints
+one JSON line.
+
+`python bench.py --gpus N` with N > 1 starts torch.distributed.run (one process
+per GPU) as a child process before touching the GPU and forwards rank 0's line
+and the exit code; under torch.distributed.run, WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -19,17 +25,34 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "mcp-raytracer_amd"))
 
-METRIC = "Msamples/sec (w×h×spp/s) Cornell 800×800 spp=256 @1/2/4/8 GPU"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+HEADLINE_METRIC = "Msamples/sec (w×h×spp/s) Cornell 800×800 spp=256 @1/2/4/8 GPU"  # BASELINE.json
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SIMDS = 1024               # 256 CUs x 4 SIMD-32
+CLOCK_GHZ = 2.4            # max engine clock (MI355X_MICROARCH.md)
+# VALU issue peak: a SIMD-32 issues one wave64 VALU instruction per 2 cycles
+# (MI355X_MICROARCH.md, wave scheduling), so 1024 x 2.4 GHz / 2 wave-instructions/s
+VALU_PEAK_GINST = SIMDS * CLOCK_GHZ / 2.0
 
 SCENES = {
-    "cornell": ({"type": "cornell"}, {}),
-    "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}}, {"aspect": 1}),
-    "rain": ({"type": "rain", "options": {"seed": 42}}, {}),
-    "default": ({"type": "default"}, {}),
+    "cornell": ({"type": "cornell"}, {}, "Cornell"),
+    "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}}, {"aspect": 1}, "spheres-500"),
+    "spheres10": ({"type": "spheres", "options": {"seed": 42}}, {"aspect": 1}, "spheres-10"),
+    "rain": ({"type": "rain", "options": {"seed": 42}}, {}, "rain-50"),
+    "default": ({"type": "default"}, {}, "default"),
     # BASELINE config 5: 100k requested, ~76.6k placed by the reference's rule
-    "spheres100k": ({"type": "spheres", "options": {"count": 100000, "seed": 42}}, {"aspect": 1}),
+    "spheres100k": ({"type": "spheres", "options": {"count": 100000, "seed": 42}}, {"aspect": 1}, "spheres-100k"),
 }
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (long runs must keep writing)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def metric_for(scene: str, W: int, H: int, spp: int, depth: int) -> str:
+    if (scene, W, H, spp, depth) == ("cornell", 800, 800, 256, 16):
+        return HEADLINE_METRIC
+    return f"Msamples/sec (w×h×spp/s) {SCENES[scene][2]} {W}×{H} spp={spp} depth={depth}"
 
 
 def algorithmic_bytes(c: dict, pixels: int) -> float:
@@ -47,24 +70,31 @@ def cpu_baseline(scene_data, ropts, width, height, spp, target_s=15.0):
     import pyoracle
 
     pyoracle.build()
+    # one short row segment sizes the sample: (cost per pixel) -> rows that fit target_s
+    seg = min(width, 64)
     t0 = time.perf_counter()
-    pyoracle.render(scene_data, ropts, region=(0, height // 2, width, 1), threads=1)
-    t_row = max(time.perf_counter() - t0, 1e-3)
-    rows = max(1, min(height, int(target_s / t_row)))
+    pyoracle.render(scene_data, ropts, region=((width - seg) // 2, height // 2, seg, 1), threads=1)
+    t_px = max(time.perf_counter() - t0, 1e-4) / seg
+    rows = max(1, min(height, int(target_s / (t_px * width))))
     step = max(1, height // rows)
+    region = None
+    if t_px * width > target_s:  # one full row is already too long: a centred row segment
+        n = max(8, int(target_s / t_px))
+        region, step = ((width - n) // 2, height // 2, n, 1), 1
     t0 = time.perf_counter()
-    out = pyoracle.render(scene_data, ropts, row_step=step, threads=1)
+    out = pyoracle.render(scene_data, ropts, row_step=step, threads=1, region=region)
     dt = time.perf_counter() - t0
     samples = out["stats"]["samples"]["total"]
+    what = (f"rows j%{step}==0 of the {width}x{height} image" if region is None
+            else f"{region[2]} px of row {region[1]}")
     line = {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"rows j%{step}==0 of the {width}x{height} image at spp={spp} "
-                      f"({int(out['stats']['pixels'])} px, {int(samples)} samples, {dt:.1f} s), "
-                      f"oracle/oracle.cpp ref precision, single thread"}
+            "sample": f"{what} at spp={spp} ({int(out['stats']['pixels'])} px, {int(samples)} samples, "
+                      f"{dt:.1f} s), oracle/oracle.cpp ref precision, single thread"}
     # the same restatement over all of this process's host cores
     # (threads over rows, the analogue of the reference's -p workers), ~target_s/2 of work.
     # The GPU box grants a 16-CPU share whatever nproc says.
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    if cores > 1:
+    if cores > 1 and region is None:
         step_mt = max(1, step * 2 // cores)
         t0 = time.perf_counter()
         out = pyoracle.render(scene_data, ropts, row_step=step_mt, threads=cores)
@@ -88,7 +118,24 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def main():
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_children(args, argv) -> int:
+    """--gpus N > 1 without a torch.distributed.run environment: run N ranks as a
+    child process (never exec from this process) and forward rank 0's output."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()), *argv]
+    log("launching " + " ".join(cmd[2:6]) + " ...")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -102,85 +149,172 @@ def main():
     ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "fast", "reference"],
                     help="closest-hit strategy (all bit-identical; auto = brute force up to 16 primitives)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-count", action="store_true", help="skip the work-counting launch (no work_rate)")
     ap.add_argument("--count-sub", type=int, default=0,
                     help="tile subsample of the work-counting launch (0 = auto: 16 above 1000 objects)")
-    ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "pmc_traffic.json"),
-                    help="JSON with measured HBM bytes per launch (from rocprofv3 --pmc)")
-    args = ap.parse_args()
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU rehearsal of the launcher and the gather (gloo, no GPU, no render: tests only)")
+    return ap.parse_args(argv)
+
+
+def _load_profile(name: str, key: str):
+    f = ROOT / "profiles" / name
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text()).get(key)
+    except Exception:
+        return None
+
+
+def roofline(cfg_key: str, build: str, samples: int, kernel_ms: float, counters, pixels: int):
+    """The dominant kernel against the bound it sits on: VALU issue.
+
+    achieved = VALU wave64 instructions per sample (rocprofv3 SQ_INSTS_VALU of
+    the same configuration and build, profiles/pmc_valu.json) x this launch's
+    samples / the launch's kernel time measured here with HIP events on the
+    launch stream; peak = 1024 SIMDs x 2.4 GHz / 2 cycles. `lane_util` (active
+    lanes per issued instruction, SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU)
+    times frac is the useful lane-issue fraction. `hbm` = the measured HBM bytes
+    of the same kernel (FETCH_SIZE x 2 + WRITE_SIZE, separate --pmc passes,
+    profiles/pmc_traffic.json) over the same time. `work_rate` = SURVEY.md §8d's
+    algorithmic bytes (L1/LDS-resident scene reads, not HBM) over the same time."""
+    k_s = kernel_ms / 1e3
+    v = _load_profile("pmc_valu.json", cfg_key)
+    t = _load_profile("pmc_traffic.json", cfg_key)
+    out = {"bound": "valu", "unit": "Ginst/s", "peak": VALU_PEAK_GINST, "kernel_ms": round(kernel_ms, 4)}
+    if v:
+        ips = v["valu_insts_per_sample"] / 64.0  # wave instructions per sample
+        ach = ips * samples / k_s / 1e9
+        out.update({"achieved": round(ach, 2), "frac": round(ach / VALU_PEAK_GINST, 4),
+                    "lane_util": v["lane_util"], "useful_lane_frac": round(ach / VALU_PEAK_GINST * v["lane_util"], 4),
+                    "valu_wave_insts_per_sample": round(ips, 2),
+                    "kernel": v["kernel"], "pmc_build": v.get("build_id"), "pmc_stale": v.get("build_id") != build,
+                    "pmc_source": "profiles/pmc_valu.json"})
+        assert out["frac"] <= 1.0, out
+    else:
+        out.update({"achieved": None, "frac": None, "pmc_source": None})
+    traffic = t.get("hbm_bytes_per_launch") if t else None
+    out["traffic"] = traffic
+    if traffic:
+        gbs = traffic / k_s / 1e9
+        out["hbm"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(gbs / HBM_PEAK_GBS, 4), "pmc_build": t.get("build_id"),
+                      "pmc_source": "profiles/pmc_traffic.json"}
+    if counters:
+        ab = algorithmic_bytes(counters, pixels)
+        out["work_rate"] = {"algorithmic_bytes_per_launch": ab, "GBps": round(ab / k_s / 1e9, 1),
+                            "note": "SURVEY.md §8d byte model of the reference algorithm (scene reads are "
+                                    "LDS/L1-resident): a work rate, not HBM traffic",
+                            "per_sample": {k: round(val / max(counters["samples"], 1), 3)
+                                           for k, val in counters.items()}}
+    return out
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_children(args, argv)
+    world_env = int(env_world or "1")
+    if world_env != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world_env} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if args.stub:
+        return stub_main(args)
 
     import torch
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
+    dev = torch.device("cuda", local_rank)
+    world = 1
+    if world_env > 1:
+        dist.init_process_group(args.backend, device_id=dev)
+        world = dist.get_world_size()  # the ranks RCCL actually connected
     from raytracer_amd import _build
 
-    if rank == 0 or world == 1:
+    if rank == 0:
         _build.build_native()
     if world > 1:
         dist.barrier()
     import raytracer_amd as rt
+    from raytracer_amd import distributed as rtd
 
-    cfg, extra = SCENES[args.scene]
+    cfg, extra, _ = SCENES[args.scene]
     scene_data = rt.generate_scene_data(cfg)
     ropts = {"width": args.width, "samples": args.spp, "depth": args.depth, "aTolerance": 0,
              "seed": args.seed, "precision": args.precision, "traversal": args.traversal, **extra}
     cam = rt.create_camera_from_scene_data(scene_data, ropts)
     W, H = cam.image_width, cam.image_height
-    dev = torch.device("cuda", local_rank)
     frame = torch.zeros((H, W, 3), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    region = (0, 0, W, H)
+    n_px = rtd.slab_tiles(region, world) * rtd.TILE_PIXELS
+    slab = torch.zeros((n_px, 3), dtype=torch.uint8, device=dev) if world > 1 else None
+    gathered = torch.zeros((world, n_px, 3), dtype=torch.uint8, device=dev) if world > 1 and rank == 0 else None
+    log(f"rank {rank}/{world}: {args.scene} {W}x{H} spp={args.spp} depth={args.depth} build {rt.build_id()}")
 
-    # Algorithmic work of this rank's launch: the node / primitive
-    # / material / light-PDF work the REFERENCE algorithm does on this workload,
+    # Algorithmic work of this rank's launch (SURVEY.md §8d): the node / primitive /
+    # material / light-PDF work the REFERENCE algorithm does on this workload,
     # counted by one instrumented, untimed launch with the reference-order
-    # traversal (its counts equal the oracle's: test_work_counters_match_oracle).
-    # Identical seeds => identical paths to every timed launch, whatever the
-    # closest-hit strategy, so this is a fixed per-workload figure.
-    # Large scenes count on a 1/count_sub tile subsample of this rank's tiles
-    # (SURVEY.md §8d's 1/16 pixel subsample) and scale to the launch.
+    # traversal (its counts equal the oracle's: test_work_counters_match_oracle),
+    # on min(spp, 64) samples and, for large scenes, a 1/count_sub tile subsample.
+    counters = None
     sub = args.count_sub or (16 if cam.info["n_objects"] > 1000 else 1)
-    st_sub, counters = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world * sub,
-                                         stream=sptr, synchronize=True, count_work=True, traversal="reference")
-    st, _ = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr,
-                              synchronize=True)
-    my_pixels = int(st.pixels)
-    scale = my_pixels / max(int(st_sub.pixels), 1)
-    counters = {k: v * scale for k, v in counters.items()}
-    bytes_per_launch = algorithmic_bytes(counters, my_pixels)
+    if not args.no_count:
+        spp_c = min(args.spp, 64)
+        cam_c = rt.create_camera_from_scene_data(scene_data, {**ropts, "samples": spp_c})
+        st_c, counters = cam_c.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world * sub,
+                                             stream=sptr, synchronize=True, count_work=True,
+                                             traversal="reference")
+        cam_c.close()
+        log(f"work counters: {int(st_c.samples['total'])} samples counted")
 
     def step():
-        frame.zero_()
-        cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr)
-        if world > 1:
-            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+        if world == 1:
+            cam.render_device(rgb_ptr=frame.data_ptr(), stream=sptr)
+        else:
+            rtd.render_frame(cam, frame, rank, world, stream=sptr, slab=slab, gathered=gathered)
 
-    for _ in range(args.warmup):
+    # this rank's share (untimed): pixels and samples per launch
+    st, _ = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr,
+                              synchronize=True)
+    my_pixels, my_samples = int(st.pixels), int(st.samples["total"])
+    if counters:
+        scale = my_samples / max(counters["samples"], 1)
+        counters = {k: v * scale for k, v in counters.items()}
+    for i in range(args.warmup):
         step()
+        torch.cuda.synchronize()
+        log(f"warmup {i + 1}/{args.warmup}")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         step()
+        if args.steps <= 5 or (i + 1) % 10 == 0:  # no sync here: keep launches queued
+            log(f"step {i + 1}/{args.steps} queued")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
     # Kernel time of the dominant kernel, from HIP events the library records on
-    # the launch stream around it (untimed steps after the timed region; each is
-    # read back before the next launch reuses the events).
+    # the launch stream (per pass, path kernel and accumulate separately), over
+    # untimed renders of this rank's share after the timed region.
     kt = []
     for _ in range(max(3, min(args.steps, 10))):
-        cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr)
+        cam.render_device(rgb_ptr=(slab if world > 1 else frame).data_ptr(), tile_group=rank, tile_groups=world,
+                          stream=sptr, packed=world > 1)
         kt.append(cam.kernel_times())
+    passes = cam.pass_count()
     kernel_ms = sum(a for a, _ in kt) / len(kt)
     accum_ms = sum(b for _, b in kt) / len(kt)
     kernel_name = "pt_chunk_kernel" if accum_ms > 0 else "pt_render_kernel"
@@ -188,43 +322,23 @@ def main():
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms_max = float(t[0]), float(t[1])
-
-    samples_per_step = W * H * args.spp
-    value = samples_per_step * args.steps / elapsed / 1e6
-    achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9  # this rank's GB/s
-    traffic = None
-    tf = Path(args.traffic_file)
-    if tf.exists():
-        try:
-            td = json.loads(tf.read_text())
-            key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n{world}"
-            traffic = td.get(key, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    # VALU evidence of the same kernel (committed rocprofv3 --pmc passes, tools/pmc_valu.sh):
-    # the path is VALU-issue / divergence bound, not HBM bound.
-    valu = None
-    vf = ROOT / "profiles" / "pmc_valu.json"
-    if vf.exists():
-        try:
-            key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n{world}"
-            e = json.loads(vf.read_text()).get(key)
-            if e:
-                valu = {k: e[k] for k in ("kernel", "valu_busy", "lane_util", "clock_ghz", "valu_insts_per_sample",
-                                          "f64_tflops", "f64_peak_tflops", "f64_frac", "duration_ms")}
-                valu["source"] = "profiles/pmc_valu.json"
-        except Exception:
-            valu = None
+    elapsed = float(t[0])
 
     if rank == 0:
+        samples_per_step = W * H * args.spp
+        value = samples_per_step * args.steps / elapsed / 1e6
+        key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n{world}"
+        rl = roofline(key, rt.build_id(), my_samples, kernel_ms, counters, my_pixels)
+        rl.update({"kernel": kernel_name, "accum_kernel_ms": round(accum_ms, 4), "passes": passes,
+                   "count_subsample": sub})
         cpu = None
         if world == 1 and not args.no_cpu:
+            log("cpu baseline")
             cpu = cpu_baseline(scene_data, {k: v for k, v in ropts.items() if k not in ("precision", "traversal")},
                                W, H, args.spp)
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
+            "metric": metric_for(args.scene, W, H, args.spp, args.depth), "value": round(value, 3),
+            "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64" if args.precision == "ref" else "f32",
@@ -232,26 +346,77 @@ def main():
                     f"{args.seed:#x}; no datasets",
             "config": {"workload": f"{args.scene} {W}x{H} spp={args.spp} depth={args.depth}",
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "depth": args.depth,
-                       "precision": args.precision, "adaptive": False, "count_subsample": sub,
+                       "precision": args.precision, "adaptive": False,
                        "traversal": ["fast", "reference", "brute"][cam.info["traversal"]],
                        "kernel": "chunked (lane work pool, in-order accumulate)" if accum_ms > 0
                                  else "sequential (wave per 8x8 tile)",
-                       "parallelism": f"8x8-tile interleave x{world} + RCCL reduce to rank 0"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": kernel_name, "kernel_ms": round(kernel_ms, 4),
-                         "accum_kernel_ms": round(accum_ms, 4),
-                         "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "work_per_sample": {k: round(v / max(counters["samples"], 1), 3)
-                                             for k, v in counters.items()}},
-            "valu": valu,
+                       "parallelism": f"8x8-tile interleave x{world}" +
+                                      (" + RCCL gather of tile-packed slabs to rank 0" if world > 1 else "")},
+            "build_id": rt.build_id(),
+            "roofline": rl,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
+
+
+def stub_main(args) -> int:
+    """CPU rehearsal (tests): the same rank bookkeeping and slab gather over
+    gloo, with a stand-in render that writes each owned pixel's own index into
+    its slab; rank 0 checks the reassembled frame and prints a line like the
+    real one. No GPU, no librt_amd.so."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from raytracer_amd import distributed as rtd
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = 1
+    if args.gpus > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    W = H = args.width
+    region = (0, 0, W, H)
+    n_px = rtd.slab_tiles(region, world) * rtd.TILE_PIXELS
+    tiles_x = -(-W // rtd.TILE)
+    slab = np.zeros((n_px, 3), np.uint8)
+    for k, g in enumerate(rtd.owned_tiles(region, rank, world)):
+        ty, tx = divmod(g, tiles_x)
+        for l in range(rtd.TILE_PIXELS):
+            i, j = tx * rtd.TILE + l % rtd.TILE, ty * rtd.TILE + l // rtd.TILE
+            if i < W and j < H:
+                slab[k * rtd.TILE_PIXELS + l] = ((j * W + i) % 251, (j * W + i) // 251 % 251, rank)
+    t0 = time.perf_counter()
+    g = rtd.gather_slabs(torch.from_numpy(slab), world)
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        frame = np.zeros((H, W, 3), np.uint8)
+        g = g.numpy()
+        for r in range(world):
+            for k, t in enumerate(rtd.owned_tiles(region, r, world)):
+                ty, tx = divmod(t, tiles_x)
+                for l in range(rtd.TILE_PIXELS):
+                    i, j = tx * rtd.TILE + l % rtd.TILE, ty * rtd.TILE + l // rtd.TILE
+                    if i < W and j < H:
+                        frame[j, i] = g[r, k * rtd.TILE_PIXELS + l]
+        idx = np.arange(W * H).reshape(H, W)
+        ok = bool((frame[..., 0] == idx % 251).all() and (frame[..., 1] == idx // 251 % 251).all())
+        owner = np.zeros((H, W), np.uint8)
+        for r in range(world):
+            owner[rtd.owner_mask(W, H, region, r, world)] = r
+        ok = ok and bool((frame[..., 2] == owner).all())
+        print(json.dumps({"metric": "stub", "value": 0.0, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 3), "stub_frame_ok": ok,
+                          "slab_bytes_per_rank": int(slab.nbytes), "frame_bytes": W * H * 3}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RT_AMD_VERSION 1
+#define RT_AMD_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -93,6 +93,10 @@ typedef struct {
     int32_t* px_bounces;     /* device W*H, may be NULL */
     void* stream;
     int32_t synchronize;     /* 1: wait and fill stats / work_counters; 0: asynchronous */
+    int32_t packed_tiles;    /* 0: outputs in full-frame layout; 1: tile-packed slab - the pixel
+                              * of lane l (= 8*row + col inside the tile) of this launch's k-th
+                              * tile at index k*64 + l (rgb/radiance 3 values per index, the
+                              * px_* arrays 1); unpack with rt_tiles_unpack (multi-GPU gather) */
 } rt_launch;
 
 /* Work counters of an instrumented launch (SURVEY.md §8d algorithmic bytes). */
@@ -164,6 +168,34 @@ int rt_device_count(int32_t* count);
  * kernel(s), `accum_ms` = the chunked mode's in-order accumulate pass (0 for the
  * sequential kernel). Waits for that call's events. */
 int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms);
+
+/* Number of chunked-kernel passes of the most recent render (0 before any; the
+ * sequential kernel counts as one). Passes split the per-sample record buffer. */
+int rt_camera_pass_count(rt_camera* cam, int32_t* passes);
+
+/* Frees the camera's device resources (scene copy, frame and record buffers,
+ * events); the next render re-creates them on the then-current device. */
+int rt_camera_release_device(rt_camera* cam);
+
+/* Hash of the HIP/C++ sources and compiler flags this library was built from
+ * (static string, never freed). */
+const char* rt_build_id(void);
+
+/* Reassembles a region's frame from tile-packed slabs (multi-GPU gather): slabs
+ * holds `tile_groups` slabs of `slab_tiles` tiles each, slab r = the packed
+ * output of tile_group r (rt_launch.packed_tiles); tile k of slab r is the
+ * region's tile r + k*tile_groups. Writes the region's pixels of `frame`
+ * (full-frame layout, width*height pixels, `channels` values of `elem_bytes`
+ * bytes each: 1 = u8 RGB, 4 = f32 radiance). DEVICE pointers; queued on
+ * `stream` (a hipStream_t, NULL = default). */
+int rt_tiles_unpack(const void* slabs, int32_t tile_groups, int32_t slab_tiles, const rt_region* region,
+                    int32_t width, int32_t height, int32_t channels, int32_t elem_bytes, void* frame, void* stream);
+
+/* Image file encoders for the framebuffer (the reference hands its buffer to
+ * sharp, src/raytracer.ts:101-110): 8-bit RGB PNG (zlib level 0-9) or binary
+ * PPM (P6). rgb: host width*height*3 bytes. *out is malloc'ed (rt_free). */
+int rt_encode_png(const uint8_t* rgb, int32_t width, int32_t height, int32_t level, uint8_t** out, size_t* out_len);
+int rt_encode_ppm(const uint8_t* rgb, int32_t width, int32_t height, uint8_t** out, size_t* out_len);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,10 @@ hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* coun
 hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float* orig, const float* dir,
                                 double* out, hipStream_t stream);
 
+// Scatter of tile-packed slabs into the full-frame layout (frame.hip).
+hipError_t launch_tiles_unpack(const void* slabs, int groups, int slab_tiles, const RtRegion& reg, int width,
+                               int channels, int elem_bytes, void* frame, hipStream_t stream);
+
 // LDS bytes per workgroup for the traversal stack (fast / reference) or the
 // per-lane candidate bounds of the nearest-first brute force.
 inline size_t stack_lds_bytes(int stack_depth, int trav, int n_prims) {

@@ -92,6 +92,9 @@ struct RenderOut {
     unsigned long long* stats;     // ST_WORDS
     unsigned long long* counters;  // kCounterWords (instrumented builds only)
     unsigned int* tile_counter;
+    // 0: outputs in full-frame layout (index j*W + i); 1: tile-packed slab, the
+    // pixel of lane l of this launch's k-th tile at k*64 + l (multi-GPU gather)
+    int32_t packed;
 };
 
 // Closest-hit strategies; all return the reference's hit bit-for-bit (see the
@@ -1562,7 +1565,8 @@ __device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, 
 struct PixStats {
     unsigned long long pixels = 0, samples = 0, smin = ~0ull, smax = 0, b = 0, bmin = ~0ull, bmax = 0;
 };
-__device__ __forceinline__ void finish_pixel(const RtCamera& C, const RenderOut& out, uint32_t pix, V3 color, int n,
+// `opix`: the pixel's output index (full-frame j*W + i, or its tile-packed slot).
+__device__ __forceinline__ void finish_pixel(const RtCamera& C, const RenderOut& out, uint32_t opix, V3 color, int n,
                                              unsigned long long bsum, int bmin, int bmax, PixStats& st) {
     V3 fin;
     if (C.mode == MODE_BOUNCES) {
@@ -1573,7 +1577,7 @@ __device__ __forceinline__ void finish_pixel(const RtCamera& C, const RenderOut&
     } else {
         fin = divs<double>(color, (double)n);
     }
-    const size_t off = (size_t)pix * 3;
+    const size_t off = (size_t)opix * 3;
     if (out.radiance) {
         out.radiance[off] = fin.x;
         out.radiance[off + 1] = fin.y;
@@ -1584,8 +1588,8 @@ __device__ __forceinline__ void finish_pixel(const RtCamera& C, const RenderOut&
         out.rgb[off + 1] = to_u8(fin.y);
         out.rgb[off + 2] = to_u8(fin.z);
     }
-    if (out.px_samples) out.px_samples[pix] = n;
-    if (out.px_bounces) out.px_bounces[pix] = (int32_t)bsum;
+    if (out.px_samples) out.px_samples[opix] = n;
+    if (out.px_bounces) out.px_bounces[opix] = (int32_t)bsum;
     st.pixels += 1;
     st.samples += (unsigned long long)n;
     st.smin = min(st.smin, (unsigned long long)n);
@@ -1750,7 +1754,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
             }
             if (PROF) pf.secs[PR_LOOP] += clk() - pf.tl;
         }
-        if (valid_px) finish_pixel(C, out, pix, color, n, bsum, bmin, bmax, st);
+        if (valid_px) finish_pixel(C, out, out.packed ? tile * kWave + (uint32_t)lane : pix, color, n, bsum, bmin, bmax, st);
     }
     publish_stats(out, st, st_err, lane);
     publish_counters<COUNT, PROF>(out, cnt, pf, lane);

@@ -94,7 +94,9 @@ __global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg
                 bmin = min(bmin, b);
                 bmax = max(bmax, b);
             }
-            finish_pixel(C, out, (uint32_t)j * (uint32_t)C.width + (uint32_t)i, color, n, bsum, bmin, bmax, st);
+            const uint32_t opix = out.packed ? (uint32_t)sb.tile0 * kWave + (uint32_t)slot
+                                             : (uint32_t)j * (uint32_t)C.width + (uint32_t)i;
+            finish_pixel(C, out, opix, color, n, bsum, bmin, bmax, st);
         }
     }
     publish_stats(out, st, 0ull, lane);

@@ -22,6 +22,10 @@
 
 using namespace rt;
 
+#ifndef RT_BUILD_ID
+#define RT_BUILD_ID "unhashed"
+#endif
+
 namespace {
 
 thread_local std::string g_error;
@@ -59,6 +63,9 @@ int device_cus(int dev) {
 }
 
 }  // namespace
+
+// error hook for the other translation units of the library (image.cpp)
+int rt_set_error_message(int code, const char* msg) { return set_error(code, msg ? msg : ""); }
 
 // ONBasis of a hit normal (src/geometry/onbasis.ts:18-51), host side: the same
 // rt_math.hpp operations as the kernel's make_onb, so the stored basis equals
@@ -106,8 +113,11 @@ struct rt_camera {
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
     int32_t n_onb = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // path start, path end, accumulate end
-    bool ev_recorded = false, ev_accum = false;
+    // HIP events of the last launch, 3 per pass: path kernel start, path kernel
+    // end, accumulate end (the sequential kernel: one pass, no accumulate)
+    std::vector<hipEvent_t> ev;
+    int n_passes = 0;
+    bool ev_accum = false;
     unsigned long long* d_stats = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned int* d_tile = nullptr;
@@ -125,11 +135,20 @@ struct rt_camera {
         for (void* p : {(void*)d_blob, (void*)d_stats, (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad,
                         (void*)d_sbuf})
             if (p) (void)hipFree(p);
-        for (hipEvent_t& e : ev)
-            if (e) (void)hipEventDestroy(e), e = nullptr;
-        ev_recorded = false;
+        // every freed pointer is reset: a later ensure_device / ensure_frame /
+        // ensure_sbuf (possibly on another device) must reallocate all of them
+        d_blob = nullptr;
+        d_stats = nullptr;
+        d_counters = nullptr;
+        d_tile = nullptr;
+        d_rgb = nullptr;
+        d_rad = nullptr;
         d_sbuf = nullptr;
         sbuf_cap = 0;
+        for (hipEvent_t& e : ev)
+            if (e) (void)hipEventDestroy(e), e = nullptr;
+        ev.clear();
+        n_passes = 0;
         (void)hipSetDevice(prev);
         device = -1;
     }
@@ -167,7 +186,6 @@ struct rt_camera {
         hip_check(hipMalloc(&d_tile, 64), "hipMalloc");
         device = dev;
         cus = device_cus(dev);
-        for (hipEvent_t& e : ev) hip_check(hipEventCreate(&e), "hipEventCreate");
         int smem = 0;
         if (hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && smem > 0)
             lds_max = smem;
@@ -178,6 +196,16 @@ struct rt_camera {
         const size_t px = (size_t)build.cam.width * build.cam.height;
         hip_check(hipMalloc(&d_rgb, std::max<size_t>(px * 3, 1)), "hipMalloc");
         hip_check(hipMalloc(&d_rad, std::max<size_t>(px * 3, 1) * sizeof(float)), "hipMalloc");
+    }
+
+    // Events of pass p (created on demand on the camera's device).
+    hipEvent_t pass_event(int p, int k) {
+        while ((int)ev.size() < 3 * (p + 1)) {
+            hipEvent_t e = nullptr;
+            hip_check(hipEventCreate(&e), "hipEventCreate");
+            ev.push_back(e);
+        }
+        return ev[3 * p + k];
     }
 
     // The strategy a launch actually uses: BRUTE/FAST are exact only where every
@@ -221,7 +249,7 @@ struct rt_camera {
 
     // Launch one render; returns after queueing (and synchronising if asked).
     void launch(const rt_region& region, int tile_group, int tile_groups, int prec, int trav, int count,
-                uint8_t* rgb, float* rad, int32_t* pxs, int32_t* pxb, hipStream_t stream) {
+                uint8_t* rgb, float* rad, int32_t* pxs, int32_t* pxb, int packed, hipStream_t stream) {
         const RtCamera& C = build.cam;
         if (tile_groups < 1 || tile_group < 0 || tile_group >= tile_groups)
             throw std::invalid_argument("tile_group must satisfy 0 <= tile_group < tile_groups");
@@ -254,9 +282,9 @@ struct rt_camera {
         g.lds_bytes = stack + (size_t)(g.lds_level == 2 ? lds_words2 : g.lds_level == 1 ? lds_words : 0) * 16;
         if (g.lds_bytes > (size_t)lds_max)
             throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
-        RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile};
+        RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile, packed ? 1 : 0};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
-        ev_recorded = false;
+        n_passes = 0;
         if (mine == 0) return;
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
@@ -271,12 +299,12 @@ struct rt_camera {
         const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 4 * resident_waves || big_scene);
         if (C.adaptive || C.n_samples <= 0 || !chunked) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
-            hip_check(hipEventRecord(ev[0], stream), "hipEventRecord");
+            hip_check(hipEventRecord(pass_event(0, 0), stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, g, nullptr, stream)
                                              : launch_render_ref(v, S, reg, out, g, nullptr, stream);
             hip_check(e, "pt_render_kernel launch");
-            hip_check(hipEventRecord(ev[1], stream), "hipEventRecord");
-            ev_recorded = true;
+            hip_check(hipEventRecord(pass_event(0, 1), stream), "hipEventRecord");
+            n_passes = 1;
             ev_accum = false;
             return;
         }
@@ -337,7 +365,8 @@ struct rt_camera {
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
         }
-        for (long t0 = 0; t0 < mine; t0 += pass_tiles) {
+        int pass = 0;
+        for (long t0 = 0; t0 < mine; t0 += pass_tiles, ++pass) {
             const long nt = std::min(pass_tiles, mine - t0);
             sb.tile0 = (int32_t)t0;
             sb.slots = (int32_t)(nt * kWave);
@@ -351,15 +380,16 @@ struct rt_camera {
             if (t0 > 0) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = g;
             gp.grid = (int)std::max<long>(1, std::min<long>(items / kBlockChunk + 1, (long)cus));
-            if (t0 == 0) hip_check(hipEventRecord(ev[0], stream), "hipEventRecord");
+            // per-pass events: path kernel [0, 1), accumulate [1, 2)
+            hip_check(hipEventRecord(pass_event(pass, 0), stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, gp, &sb, stream)
                                              : launch_render_ref(v, S, reg, out, gp, &sb, stream);
             hip_check(e, "pt_chunk_kernel launch");
-            if (t0 + pass_tiles >= mine) hip_check(hipEventRecord(ev[1], stream), "hipEventRecord");
+            hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
             hip_check(launch_accum(S, reg, out, g.tiles_x, sb, stream), "pt_accum_kernel launch");
+            hip_check(hipEventRecord(pass_event(pass, 2), stream), "hipEventRecord");
         }
-        hip_check(hipEventRecord(ev[2], stream), "hipEventRecord");
-        ev_recorded = true;
+        n_passes = pass;
         ev_accum = true;
     }
 
@@ -536,7 +566,7 @@ int rt_camera_render_region(rt_camera* cam, const rt_region* region, uint8_t* rg
         const RtCamera& C = cam->build.cam;
         const hipStream_t stream = nullptr;
         cam->launch(*region, 0, 1, cam->precision, cam->traversal, 0, rgb ? cam->d_rgb : nullptr,
-                    radiance ? cam->d_rad : nullptr, nullptr, nullptr, stream);
+                    radiance ? cam->d_rad : nullptr, nullptr, nullptr, 0, stream);
         cam->read_stats(stats, nullptr, stream);
         // copy back only the region's rows/columns (the caller's buffer is the full frame)
         const int x0 = std::max(region->x, 0), y0 = std::max(region->y, 0);
@@ -580,7 +610,7 @@ int rt_camera_render_device(rt_camera* cam, const rt_launch* L, rt_render_stats*
         const int trav = L->traversal < 0 ? cam->traversal : L->traversal;
         if (L->count_work < 0 || L->count_work > 2) throw std::invalid_argument("count_work must be 0, 1 or 2");
         cam->launch(L->region, L->tile_group, L->tile_groups, prec, trav, L->count_work, L->rgb, L->radiance,
-                    L->px_samples, L->px_bounces, stream);
+                    L->px_samples, L->px_bounces, L->packed_tiles, stream);
         if (L->synchronize) cam->read_stats(stats, L->count_work ? work_counters : nullptr, stream);
         return RT_OK;
     } catch (const HipError& e) {
@@ -654,14 +684,59 @@ int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms) {
     try {
         *path_ms = 0.0f;
         *accum_ms = 0.0f;
-        if (!cam->ev_recorded) return RT_OK;
-        hip_check(hipEventSynchronize(cam->ev[1]), "hipEventSynchronize");
-        hip_check(hipEventElapsedTime(path_ms, cam->ev[0], cam->ev[1]), "hipEventElapsedTime");
-        if (cam->ev_accum) {
-            hip_check(hipEventSynchronize(cam->ev[2]), "hipEventSynchronize");
-            hip_check(hipEventElapsedTime(accum_ms, cam->ev[1], cam->ev[2]), "hipEventElapsedTime");
+        // summed per pass: path kernel time and accumulate time, never one span across both
+        for (int p = 0; p < cam->n_passes; ++p) {
+            float a = 0.0f, b = 0.0f;
+            hip_check(hipEventSynchronize(cam->ev[3 * p + 1]), "hipEventSynchronize");
+            hip_check(hipEventElapsedTime(&a, cam->ev[3 * p], cam->ev[3 * p + 1]), "hipEventElapsedTime");
+            *path_ms += a;
+            if (cam->ev_accum) {
+                hip_check(hipEventSynchronize(cam->ev[3 * p + 2]), "hipEventSynchronize");
+                hip_check(hipEventElapsedTime(&b, cam->ev[3 * p + 1], cam->ev[3 * p + 2]), "hipEventElapsedTime");
+                *accum_ms += b;
+            }
         }
         return RT_OK;
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_DEVICE, e.what());
+    }
+}
+
+int rt_camera_pass_count(rt_camera* cam, int32_t* passes) {
+    if (!cam || !passes) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    *passes = cam->n_passes;
+    return RT_OK;
+}
+
+int rt_camera_release_device(rt_camera* cam) {
+    if (!cam) return set_error(RT_ERR_INVALID, "null camera");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    cam->release();
+    return RT_OK;
+}
+
+const char* rt_build_id(void) { return RT_BUILD_ID; }
+
+int rt_tiles_unpack(const void* slabs, int32_t tile_groups, int32_t slab_tiles, const rt_region* region,
+                    int32_t width, int32_t height, int32_t channels, int32_t elem_bytes, void* frame, void* stream) {
+    if (!region || tile_groups < 1 || slab_tiles < 0 || width < 0 || height < 0 || channels < 1 ||
+        (elem_bytes != 1 && elem_bytes != 4) || (slab_tiles > 0 && (!slabs || !frame)))
+        return set_error(RT_ERR_INVALID, "rt_tiles_unpack: bad arguments");
+    try {
+        // the region clamped to the image, as the render launch clamps it
+        const int x0 = std::max(region->x, 0), y0 = std::max(region->y, 0);
+        const int x1 = std::min(region->x + region->width, width), y1 = std::min(region->y + region->height, height);
+        const RtRegion reg{x0, y0, std::max(x1 - x0, 0), std::max(y1 - y0, 0), 0, 1};
+        const long tiles = (long)((reg.width + kTile - 1) / kTile) * ((reg.height + kTile - 1) / kTile);
+        if ((long)slab_tiles * tile_groups < tiles)
+            throw std::invalid_argument("rt_tiles_unpack: slabs hold fewer tiles than the region");
+        hip_check(launch_tiles_unpack(slabs, tile_groups, slab_tiles, reg, width, channels, elem_bytes, frame,
+                                      (hipStream_t)stream),
+                  "tiles_unpack_kernel");
+        return RT_OK;
+    } catch (const std::invalid_argument& e) {
+        return set_error(RT_ERR_INVALID, e.what());
     } catch (const std::exception& e) {
         return set_error(RT_ERR_DEVICE, e.what());
     }

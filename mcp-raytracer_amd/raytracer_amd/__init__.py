@@ -9,14 +9,14 @@ This package is the host-side mirror of the reference's TypeScript surface:
     Camera.render_region / Camera.render -> RenderStats                  (src/camera.ts)
     generate_image_buffer                                                (src/raytracer.ts)
 """
-from ._lib import RtError, device_count
+from ._lib import RtError, build_id, device_count
 from .camera import Camera, RenderStats, rng_stream
 from .raytracer import divide_into_regions, divideIntoRegions, generate_image_buffer, generateImageBuffer
 from .scenes import (create_camera_from_scene_data, createCameraFromSceneData, generate_scene,
                      generate_scene_data, generateScene, generateSceneData)
 
 __all__ = [
-    "Camera", "RenderStats", "RtError", "device_count", "rng_stream",
+    "Camera", "RenderStats", "RtError", "build_id", "device_count", "rng_stream",
     "generate_scene_data", "create_camera_from_scene_data", "generate_scene",
     "generate_image_buffer", "divide_into_regions",
     "generateSceneData", "createCameraFromSceneData", "generateScene", "generateImageBuffer",

@@ -7,9 +7,11 @@ never fuses); the fp32 fast-mode TU may fuse.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -36,10 +38,29 @@ _KERNEL_FLAGS = ["-fno-slp-vectorize"]
 _UNITS = [
     ("pt_ref.hip", ["-ffp-contract=off", *_KERNEL_FLAGS], True),
     ("pt_fp32.hip", ["-ffp-contract=fast", *_KERNEL_FLAGS], True),
+    ("frame.hip", [], True),
     ("rt_api.cpp", ["-ffp-contract=off", "-x", "hip"], True),
     ("scene.cpp", ["-ffp-contract=off"], False),
+    ("image.cpp", [], False),
 ]
 _HEADERS = ["json.hpp", "rt_math.hpp", "scene.hpp", "pt_kernel.hpp", "launch.hpp"]
+_LIBS = ["-lz"]
+
+
+def source_hash(defines=(), flags=()) -> str:
+    """Build id: sha256 of every source and header the library is compiled from
+    plus the compiler flags (16 hex digits). Embedded in librt_amd.so
+    (rt_build_id) and written next to it, so a stale binary is never reused."""
+    h = hashlib.sha256()
+    for name in [u[0] for u in _UNITS] + _HEADERS:
+        h.update(name.encode() + b"\0" + (CSRC / name).read_bytes())
+    h.update((INCLUDE / "rt_amd.h").read_bytes())
+    h.update(repr((ARCH, _COMMON[:3], [(u[0], u[1]) for u in _UNITS], _LIBS, list(defines), list(flags))).encode())
+    return h.hexdigest()[:16]
+
+
+def id_path(lib_path: Path) -> Path:
+    return lib_path.with_name(lib_path.name + ".id")
 
 
 def hipcc() -> str:
@@ -49,39 +70,42 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP toolchain is required to build librt_amd.so")
 
 
-def _newest_input() -> float:
-    paths = [CSRC / u[0] for u in _UNITS] + [CSRC / h for h in _HEADERS] + [INCLUDE / "rt_amd.h", Path(__file__)]
-    return max(p.stat().st_mtime for p in paths)
-
-
 def build_native(force: bool = False, verbose: bool = False, variant: str = "", defines=(), flags=()) -> Path:
     """Compile (if stale) and return the path of librt_amd.so. `variant` + `defines`
     (+ extra compiler `flags`) build an experimental lib/librt_amd_<variant>.so
     (loaded with RT_AMD_VARIANT)."""
     lib_path = LIB_PATH.with_name(f"librt_amd_{variant}.so") if variant else LIB_PATH
-    if not force and lib_path.exists() and lib_path.stat().st_mtime >= _newest_input():
+    bid = source_hash(defines, flags)
+    idp = id_path(lib_path)
+    if not force and lib_path.exists() and idp.exists() and idp.read_text().strip() == bid:
         return lib_path
     cc = hipcc()
     obj_dir = OBJ_DIR / variant if variant else OBJ_DIR
     obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
-    objs = []
+    cmds, objs = [], []
     for src, uflags, is_hip in _UNITS:
         obj = obj_dir / (src.replace(".", "_") + ".o")
-        cmd = [cc, *_COMMON, *uflags, *flags, *[f"-D{d}" for d in defines]]
+        cmd = [cc, *_COMMON, *uflags, *flags, *[f"-D{d}" for d in defines], f'-DRT_BUILD_ID="{bid}"']
         if is_hip:
             cmd.append(f"--offload-arch={ARCH}")
         cmd += ["-c", str(CSRC / src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        cmds.append(cmd)
         objs.append(str(obj))
+    # the units compile independently: in parallel (the kernel units dominate)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1)))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
+            f.result()
     tmp = lib_path.with_suffix(".so.tmp")
-    cmd = [cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *objs]
+    cmd = [cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *objs, *_LIBS]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, lib_path)
+    idp.write_text(bid + "\n")
     return lib_path
 
 

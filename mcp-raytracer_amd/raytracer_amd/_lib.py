@@ -11,7 +11,7 @@ import json
 import os
 from pathlib import Path
 
-from ._build import LIB_PATH
+from ._build import LIB_PATH, id_path, source_hash
 
 # Public header, parsed by tests to check that every declared symbol is exported.
 HEADER = Path(__file__).resolve().parents[2] / "include" / "rt_amd.h"
@@ -54,7 +54,7 @@ class RtLaunch(C.Structure):
                 ("precision", C.c_int32), ("traversal", C.c_int32), ("count_work", C.c_int32),
                 ("rgb", C.c_void_p), ("radiance", C.c_void_p),
                 ("px_samples", C.c_void_p), ("px_bounces", C.c_void_p),
-                ("stream", C.c_void_p), ("synchronize", C.c_int32)]
+                ("stream", C.c_void_p), ("synchronize", C.c_int32), ("packed_tiles", C.c_int32)]
 
 
 class RtError(RuntimeError):
@@ -85,6 +85,14 @@ _SIGS = {
     "rt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_void_p]),
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "rt_camera_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "rt_camera_pass_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    "rt_camera_release_device": (C.c_int, [C.c_void_p]),
+    "rt_build_id": (C.c_char_p, []),
+    "rt_tiles_unpack": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(RtRegion), C.c_int32, C.c_int32,
+                                  C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "rt_encode_png": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p),
+                                C.POINTER(C.c_size_t)]),
+    "rt_encode_ppm": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
 }
 
 _lib = None
@@ -117,8 +125,19 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # the binary must have been built from these sources (no stale .so under test)
+    built = lib.rt_build_id().decode()
+    want = source_hash() if not variant else (id_path(path).read_text().strip() if id_path(path).exists() else "")
+    if built != want:
+        raise ImportError(f"{path.name} was built from sources {built}, the tree has {want}: "
+                          "rebuild with __graft_entry__.build()")
     _lib = lib
     return lib
+
+
+def build_id() -> str:
+    """Source hash librt_amd.so was built from (rt_build_id)."""
+    return load().rt_build_id().decode()
 
 
 def check(code: int) -> None:

@@ -147,9 +147,11 @@ class Camera:
 
     def render_device(self, *, rgb_ptr=None, radiance_ptr=None, region=None, tile_group=0, tile_groups=1,
                       precision: Optional[str] = None, stream=None, synchronize=False, count_work=False,
-                      px_samples_ptr=None, px_bounces_ptr=None, traversal: Optional[str] = None):
+                      px_samples_ptr=None, px_bounces_ptr=None, traversal: Optional[str] = None,
+                      packed: bool = False):
         """Device-resident render into caller-owned device buffers (full-frame
-        layout). Returns (RenderStats|None, work_counters|None)."""
+        layout, or with `packed` the tile-packed slab layout of rt_launch).
+        Returns (RenderStats|None, work_counters|None)."""
         if region is None:
             region = (0, 0, self.image_width, self.image_height)
         L = _lib.RtLaunch()
@@ -165,6 +167,7 @@ class Camera:
         L.px_bounces = px_bounces_ptr
         L.stream = stream
         L.synchronize = 1 if synchronize else 0
+        L.packed_tiles = 1 if packed else 0
         st = _lib.RtRenderStats()
         cnt = (C.c_uint64 * _lib.COUNTER_WORDS)()
         _lib.check(self._lib.rt_camera_render_device(self._h, C.byref(L), C.byref(st), cnt))
@@ -182,6 +185,16 @@ class Camera:
         a, b = C.c_float(), C.c_float()
         _lib.check(self._lib.rt_camera_kernel_times(self._h, C.byref(a), C.byref(b)))
         return float(a.value), float(b.value)
+
+    def pass_count(self) -> int:
+        """Chunked-kernel passes of the last render (rt_camera_pass_count)."""
+        n = C.c_int32()
+        _lib.check(self._lib.rt_camera_pass_count(self._h, C.byref(n)))
+        return int(n.value)
+
+    def release_device(self) -> None:
+        """Free the device copies; the next render re-creates them (rt_camera_release_device)."""
+        _lib.check(self._lib.rt_camera_release_device(self._h))
 
     # -- introspection (tests) -----------------------------------------------
     def export(self):

@@ -1,30 +1,45 @@
-"""PNG encoding of the raw RGB framebuffer.
+"""Image files from the raw RGB framebuffer.
 
 The reference hands its Uint8ClampedArray to sharp/libvips
-(src/raytracer.ts:101-110). That step is outside the hot path; this is a
-dependency-free encoder (8-bit RGB, filter 0, zlib) producing an equivalent
-PNG of the same pixels.
+(src/raytracer.ts:101-110). Encoding runs in librt_amd.so (rt_encode_png:
+8-bit RGB, filter 0 rows, zlib; rt_encode_ppm: binary P6) right next to the
+u8 frame the device wrote; decode_png_rgb is a minimal reader for tests.
 """
 from __future__ import annotations
 
+import ctypes as C
 import struct
 import zlib
 
-
-def _chunk(tag: bytes, data: bytes) -> bytes:
-    return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+from . import _lib
 
 
-def encode_png(rgb, width: int, height: int, channels: int = 3) -> bytes:
+def _call(fn, *args) -> bytes:
+    out, n = C.c_void_p(), C.c_size_t()
+    _lib.check(fn(*args, C.byref(out), C.byref(n)))
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        _lib.load().rt_free(out)
+
+
+def _buf(rgb, width: int, height: int, channels: int):
     if channels != 3:
         raise ValueError("only RGB is supported")
     raw = bytes(rgb)
     if len(raw) < width * height * 3:
         raise ValueError("pixel buffer too small")
-    stride = width * 3
-    rows = b"".join(b"\x00" + raw[y * stride:(y + 1) * stride] for y in range(height))
-    ihdr = struct.pack(">IIBBBBB", width, height, 8, 2, 0, 0, 0)
-    return b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", ihdr) + _chunk(b"IDAT", zlib.compress(rows, 6)) + _chunk(b"IEND", b"")
+    return raw
+
+
+def encode_png(rgb, width: int, height: int, channels: int = 3, level: int = 6) -> bytes:
+    raw = _buf(rgb, width, height, channels)
+    return _call(_lib.load().rt_encode_png, raw, width, height, level)
+
+
+def encode_ppm(rgb, width: int, height: int, channels: int = 3) -> bytes:
+    raw = _buf(rgb, width, height, channels)
+    return _call(_lib.load().rt_encode_ppm, raw, width, height)
 
 
 def decode_png_rgb(png: bytes):
@@ -35,6 +50,8 @@ def decode_png_rgb(png: bytes):
         (n,) = struct.unpack(">I", png[pos:pos + 4])
         tag = png[pos + 4:pos + 8]
         data = png[pos + 8:pos + 8 + n]
+        (crc,) = struct.unpack(">I", png[pos + 8 + n:pos + 12 + n])
+        assert crc == zlib.crc32(tag + data) & 0xFFFFFFFF, tag
         if tag == b"IHDR":
             w, h = struct.unpack(">II", data[:8])
         elif tag == b"IDAT":

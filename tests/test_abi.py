@@ -11,10 +11,17 @@ def test_library_exports_every_declared_symbol(rt):
     lib = _lib.load()
     text = _lib.HEADER.read_text()
     names = set(re.findall(r"^\s*(?:int|void|const char\*)\s+\**(rt_\w+)\s*\(", text, re.M))
-    assert len(names) >= 14
+    assert len(names) >= 20
     for n in sorted(names):
         assert hasattr(lib, n), f"{n} declared in rt_amd.h but not exported"
-    assert lib.rt_version() == 1
+    assert lib.rt_version() == 2
+
+
+def test_build_id_matches_sources(rt):
+    """The loaded librt_amd.so was compiled from this tree's sources and flags."""
+    from raytracer_amd import _build
+    assert rt.build_id() == _build.source_hash()
+    assert len(rt.build_id()) == 16
 
 
 def test_library_is_gfx950_code_object(rt):
@@ -96,12 +103,29 @@ def test_metal_fuzz_and_mixed_weight_clamps(rt):
     assert list(mixed["emitted"][0][:3]) == [2.0, 2.0, 2.0]  # E1*0 + E2*(1-0)
 
 
-def test_png_encoder_roundtrip():
+def test_png_encoder_roundtrip(rt):
+    """rt_encode_png (librt_amd.so): 8-bit RGB, filter 0, zlib; CRCs checked by the decoder."""
     from raytracer_amd.png import decode_png_rgb, encode_png
     import numpy as np
     px = (np.arange(5 * 3 * 3) % 251).astype(np.uint8)
-    w, h, out = decode_png_rgb(encode_png(px.tobytes(), 5, 3))
-    assert (w, h) == (5, 3) and out == px.tobytes()
+    for level in (0, 6, 9):
+        w, h, out = decode_png_rgb(encode_png(px.tobytes(), 5, 3, level=level))
+        assert (w, h) == (5, 3) and out == px.tobytes()
+    big = np.random.default_rng(0).integers(0, 256, (300, 211, 3), dtype=np.uint8)
+    w, h, out = decode_png_rgb(encode_png(big.tobytes(), 211, 300))
+    assert (w, h) == (211, 300) and out == big.tobytes()
+    with pytest.raises(ValueError):
+        encode_png(b"\0" * 10, 5, 3)
+    with pytest.raises(rt.RtError):
+        encode_png(px.tobytes(), 5, 3, level=11)
+
+
+def test_ppm_encoder(rt):
+    from raytracer_amd.png import encode_ppm
+    import numpy as np
+    px = (np.arange(4 * 2 * 3) % 251).astype(np.uint8)
+    out = encode_ppm(px.tobytes(), 4, 2)
+    assert out == b"P6\n4 2\n255\n" + px.tobytes()
 
 
 def test_divide_into_regions_matches_reference(rt):

@@ -1,16 +1,23 @@
-"""Multi-rank partition and framebuffer assembly on CPU (gloo, world_size 2).
+"""Multi-rank partition and framebuffer gather on CPU (gloo, world_size 2).
 
-The GPU render of each rank's tiles is stood in for by the oracle's image
-(no GPU here); what is under test is the product's tile ownership
-(raytracer_amd.distributed.owner_mask, the kernel's tile walk) and the
-reduce-to-rank-0 assembly (assemble_on_root), the same code bench.py runs
-over RCCL.
+The GPU render of each rank's tiles is stood in for by packing the oracle's
+image into the tile-packed slab layout (no GPU here; the packed kernel output
+is checked against the same layout on the GPU in test_gpu_parity.py); what is
+under test is the product's tile ownership (raytracer_amd.distributed) and
+the slab gather to rank 0 (gather_slabs), the same code bench.py runs over
+RCCL, plus bench.py's multi-process launcher.
 """
+import json
 import os
 import socket
+import subprocess
+import sys
+from pathlib import Path
 
 import numpy as np
 import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
 
 
 def _free_port():
@@ -31,27 +38,75 @@ def test_owner_masks_partition_the_image(W, H, world):
     assert cover[2:H - 1, 3:W - 2].min() == 1 and cover.sum() == (W - 5) * (H - 3)
 
 
+def pack_np(img, region, rank, world):
+    """Restatement of the kernels' packed output: owned tile k, lane l -> k*64 + l."""
+    from raytracer_amd import distributed as rtd
+    H, W = img.shape[:2]
+    x, y, w, h = rtd.clamp_region(region, W, H)
+    tiles_x = -(-w // 8)
+    slab = np.zeros((rtd.slab_tiles((x, y, w, h), world) * 64, *img.shape[2:]), img.dtype)
+    for k, t in enumerate(rtd.owned_tiles((x, y, w, h), rank, world)):
+        ty, tx = divmod(t, tiles_x)
+        for l in range(64):
+            i, j = x + tx * 8 + l % 8, y + ty * 8 + l // 8
+            if i < x + w and j < y + h:
+                slab[k * 64 + l] = img[j, i]
+    return slab
+
+
+def unpack_np(slabs, region, W, H, frame):
+    """Restatement of rt_tiles_unpack (frame.hip)."""
+    from raytracer_amd import distributed as rtd
+    x, y, w, h = rtd.clamp_region(region, W, H)
+    world = slabs.shape[0]
+    for r in range(world):
+        tiles_x = -(-w // 8)
+        for k, t in enumerate(rtd.owned_tiles((x, y, w, h), r, world)):
+            ty, tx = divmod(t, tiles_x)
+            for l in range(64):
+                i, j = x + tx * 8 + l % 8, y + ty * 8 + l // 8
+                if i < x + w and j < y + h:
+                    frame[j, i] = slabs[r, k * 64 + l]
+    return frame
+
+
+def test_pack_unpack_roundtrip():
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 255, (21, 37, 3), dtype=np.uint8)
+    for world in (1, 2, 3, 5):
+        for region in [(0, 0, 37, 21), (3, 2, 30, 40)]:
+            slabs = np.stack([pack_np(img, region, r, world) for r in range(world)])
+            out = unpack_np(slabs, region, 37, 21, np.zeros_like(img))
+            from raytracer_amd.distributed import clamp_region
+            x, y, w, h = clamp_region(region, 37, 21)
+            assert np.array_equal(out[y:y + h, x:x + w], img[y:y + h, x:x + w])
+            assert out.sum() == img[y:y + h, x:x + w].sum()
+
+
 def _worker(rank, world, port, full_rgb, full_rad, q):
     import torch
     import torch.distributed as dist
-    from raytracer_amd.distributed import assemble_on_root, owner_mask
+    from raytracer_amd.distributed import gather_slabs, slab_tiles
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     H, W = full_rgb.shape[:2]
-    m = owner_mask(W, H, (0, 0, W, H), rank, world)
-    frame = torch.zeros((H, W, 3), dtype=torch.uint8)
-    rad = torch.zeros((H, W, 3), dtype=torch.float32)
-    frame[torch.from_numpy(m)] = torch.from_numpy(full_rgb)[torch.from_numpy(m)]
-    rad[torch.from_numpy(m)] = torch.from_numpy(full_rad)[torch.from_numpy(m)]
-    assemble_on_root(frame)
-    assemble_on_root(rad)
+    region = (0, 0, W, H)
+    slab = torch.from_numpy(pack_np(full_rgb, region, rank, world))
+    rslab = torch.from_numpy(pack_np(full_rad, region, rank, world))
+    assert slab.shape[0] == slab_tiles(region, world) * 64
+    g = gather_slabs(slab, world)
+    gr = gather_slabs(rslab, world)
     if rank == 0:
-        q.put((frame.numpy().copy(), rad.numpy().copy()))
+        rgb = unpack_np(g.numpy(), region, W, H, np.zeros_like(full_rgb))
+        rad = unpack_np(gr.numpy(), region, W, H, np.zeros_like(full_rad))
+        q.put((rgb, rad, int(slab.numel())))
+    else:
+        assert g is None
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_two_rank_assembly_equals_full_render(oracle, rt):
+def test_gloo_two_rank_gather_equals_full_render(oracle, rt):
     import torch.multiprocessing as mp
     sd = rt.generate_scene_data({"type": "cornell"})
     full = oracle.render(sd, {"width": 40, "samples": 4, "depth": 6, "aTolerance": 0})
@@ -61,9 +116,40 @@ def test_gloo_two_rank_assembly_equals_full_render(oracle, rt):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, full["rgb"], full["radiance"], q)) for r in range(2)]
     for p in procs:
         p.start()
-    rgb, rad = q.get(timeout=120)
+    rgb, rad, slab_elems = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert np.array_equal(rgb, full["rgb"])
-    assert np.array_equal(rad, full["radiance"])  # x + 0 == x: the reduce is exact
+    assert np.array_equal(rad, full["radiance"])
+    assert slab_elems == 13 * 64 * 3  # 25 tiles over 2 ranks: frame/world (+ padding), not a full frame
+
+
+def _bench(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                          env=env, timeout=timeout, cwd=str(ROOT))
+
+
+def test_bench_launcher_spawns_world_two():
+    """bench.py --gpus 2 (no torch.distributed.run env): starts 2 ranks as a child
+    process and forwards rank 0's line; the ranks really gathered (gloo stub)."""
+    r = _bench(["--gpus", "2", "--stub", "--width", "37", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["stub_frame_ok"] is True
+    assert lines[0]["slab_bytes_per_rank"] < lines[0]["frame_bytes"]
+
+
+def test_bench_world_size_mismatch_fails():
+    r = _bench(["--gpus", "4", "--stub"], env_extra={"WORLD_SIZE": "2"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_metric_names_the_workload():
+    import bench
+    assert bench.metric_for("cornell", 800, 800, 256, 16) == bench.HEADLINE_METRIC
+    m = bench.metric_for("spheres100k", 4096, 4096, 1024, 100)
+    assert "spheres-100k" in m and "4096×4096" in m and "spp=1024" in m

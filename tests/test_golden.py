@@ -46,7 +46,8 @@ def test_gpu_reproduces_golden(rt, gpu, name):
     rgb = np.zeros((H, W, 3), np.uint8)
     rad = np.zeros((H, W, 3), np.float32)
     cam.render(rgb, radiance=rad)
-    eq = float((rgb == z["rgb"]).all(axis=-1).mean())
-    close = float(np.isclose(rad, z["radiance"], rtol=1e-6, atol=1e-6, equal_nan=True).all(axis=-1).mean())
-    print(f"{name}: rgb equal {eq:.5f} radiance equal {close:.5f}")
-    assert eq >= 0.995 and close >= 0.995
+    # bit-identity: every pixel, u8 and fp32 radiance
+    n_rgb = int((rgb != z["rgb"]).any(axis=-1).sum())
+    n_rad = int((~((rad == z["radiance"]) | (np.isnan(rad) & np.isnan(z["radiance"])))).any(axis=-1).sum())
+    print(f"{name}: pixels differing rgb {n_rgb}, radiance {n_rad}")
+    assert n_rgb == 0 and n_rad == 0, (name, n_rgb, n_rad)
