@@ -108,13 +108,16 @@ enum {
     RT_CT_WORDS
 };
 /* count_work == 2 (diagnostic): wave-cycles (s_memtime) per path-loop section,
- * summed over waves, at work_counters[RT_CT_WORDS + RT_PR_*]. */
+ * summed over waves, at work_counters[RT_CT_WORDS + RT_PR_*]; for sections
+ * k < RT_PR_LOOP also the active lanes summed over the wave executions of the
+ * section at [RT_CT_WORDS + RT_PR_WORDS + k] and the number of those executions
+ * at [RT_CT_WORDS + RT_PR_WORDS + RT_PR_LOOP + k]. */
 enum {
     RT_PR_NEWPATH = 0, RT_PR_RR, RT_PR_HIT, RT_PR_MISS, RT_PR_HITREC, RT_PR_SCATTER, RT_PR_SAMPLE, RT_PR_PDF,
     RT_PR_ACC, RT_PR_TILE, RT_PR_LOOP, RT_PR_TRIPS, RT_PR_WORDS
 };
 /* work_counters arrays passed to rt_camera_render_device hold this many entries. */
-#define RT_COUNTER_WORDS 32
+#define RT_COUNTER_WORDS 64
 
 int rt_version(void);
 const char* rt_last_error(void);

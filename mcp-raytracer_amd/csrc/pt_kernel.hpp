@@ -82,7 +82,11 @@ enum {
     PR_NEWPATH = 0, PR_RR, PR_HIT, PR_MISS, PR_HITREC, PR_SCATTER, PR_SAMPLE, PR_PDF, PR_ACC, PR_TILE, PR_LOOP,
     PR_TRIPS, PR_WORDS
 };
-constexpr int kCounterWords = 32;  // CT_WORDS + PR_WORDS, rounded up
+// INSTR == 2 also records, per section k < PR_LOOP, the lanes active when a wave
+// ended it (summed, at CT_WORDS + PR_WORDS + k) and how many times a wave did
+// (at CT_WORDS + PR_WORDS + PR_LOOP + k): active lanes per execution of a section.
+constexpr int kCounterWords = 64;  // CT_WORDS + PR_WORDS + 2 * PR_LOOP, rounded up
+static_assert(CT_WORDS + PR_WORDS + 2 * PR_LOOP <= kCounterWords, "counter words");
 
 struct RenderOut {
     uint8_t* rgb;        // W*H*3 (full frame layout), may be null
@@ -1341,6 +1345,7 @@ __device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_
 // Diagnostic section timer (INSTR == 2): wave-cycles per path-loop section.
 struct Prof {
     unsigned long long secs[PR_WORDS];
+    uint32_t lanes[PR_LOOP], execs[PR_LOOP];  // active lanes / wave executions per section (first active lane)
     unsigned long long tt, tl;
 };
 template <bool PROF>
@@ -1349,6 +1354,13 @@ __device__ __forceinline__ void psec(Prof& pf, int k) {
         const unsigned long long n = clk();
         pf.secs[k] += n - pf.tt;
         pf.tt = n;
+        if (k < PR_LOOP) {
+            const unsigned long long m = __ballot(1);
+            if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) {
+                pf.lanes[k] += (uint32_t)__popcll(m);
+                pf.execs[k] += 1u;
+            }
+        }
     }
 }
 
@@ -1635,6 +1647,15 @@ __device__ __forceinline__ void publish_counters(const RenderOut& out, const uin
 #pragma unroll
         for (int k = 0; k < PR_WORDS; ++k)
             if (lane == 0) atomicAdd(&out.counters[CT_WORDS + k], pf.secs[k]);
+#pragma unroll
+        for (int k = 0; k < PR_LOOP; ++k) {
+            const unsigned long long l = wave_sum((unsigned long long)pf.lanes[k]);
+            const unsigned long long e = wave_sum((unsigned long long)pf.execs[k]);
+            if (lane == 0) {
+                atomicAdd(&out.counters[CT_WORDS + PR_WORDS + k], l);
+                atomicAdd(&out.counters[CT_WORDS + PR_WORDS + PR_LOOP + k], e);
+            }
+        }
     }
 }
 
@@ -1698,6 +1719,8 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
     if (PROF) {
 #pragma unroll
         for (int k = 0; k < PR_WORDS; ++k) pf.secs[k] = 0;
+#pragma unroll
+        for (int k = 0; k < PR_LOOP; ++k) pf.lanes[k] = pf.execs[k] = 0u;
         pf.tt = clk();
     }
 
@@ -1836,6 +1859,8 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     if (PROF) {
 #pragma unroll
         for (int k = 0; k < PR_WORDS; ++k) pf.secs[k] = 0;
+#pragma unroll
+        for (int k = 0; k < PR_LOOP; ++k) pf.lanes[k] = pf.execs[k] = 0u;
         pf.tt = clk();
     }
 
@@ -1895,6 +1920,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 pool_next += take;
             }
         }
+        psec<PROF>(pf, PR_TILE);  // the item hand-out (wave-uniform)
         if (__ballot(slot >= 0) == 0ull) {
             if (exhausted) break;
             continue;
@@ -1941,8 +1967,8 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             if (new_path) {
                 path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)s);
                 new_path = false;
+                psec<PROF>(pf, PR_NEWPATH);
             }
-            psec<PROF>(pf, PR_NEWPATH);
             V3 c;
             if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(S, C, P, stk, stkt, cnt, st_err, pf, c)) {
                 float4 r;

@@ -23,7 +23,7 @@ TRAVERSAL = {"fast": 0, "reference": 1, "brute": 2, "auto": 3}
 CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_sphere",
             "bounces", "diffuse", "samples", "rays", "exact", "exact_wave"]
 PR_NAMES = ["newpath", "rr", "hit", "miss", "hitrec", "scatter", "sample", "pdf", "acc", "tile", "loop", "trips"]
-COUNTER_WORDS = 32
+COUNTER_WORDS = 64
 
 
 class RtRegion(C.Structure):

@@ -176,6 +176,11 @@ class Camera:
         if count_work == "profile":
             base = len(_lib.CT_NAMES)
             counters = {k: int(cnt[base + i]) for i, k in enumerate(_lib.PR_NAMES)}
+            nl = _lib.PR_NAMES.index("loop")
+            lb = base + len(_lib.PR_NAMES)
+            for i, k in enumerate(_lib.PR_NAMES[:nl]):
+                counters[f"lanes_{k}"] = int(cnt[lb + i])
+                counters[f"execs_{k}"] = int(cnt[lb + nl + i])
         else:
             counters = dict(zip(_lib.CT_NAMES, [int(v) for v in cnt])) if count_work else None
         return RenderStats._from_c(st), counters

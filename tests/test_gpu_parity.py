@@ -572,7 +572,7 @@ def test_config1_spheres10_full_frame_matches_oracle(rt, oracle, gpu):
     200x200, spp 4, depth 4 (src/benchmark.ts:25-97, scenes-spheres.ts:32) -
     the whole frame against the oracle, bit for bit."""
     sd = rt.generate_scene_data({"type": "spheres", "options": {"seed": 42}})
-    assert len(sd["objects"]) == 11  # 10 spheres + the ground
+    assert len(sd["objects"]) == 10  # count 10 (scenes-spheres.ts:32)
     ro = {"width": 200, "aspect": 1, "samples": 4, "depth": 4, **NOADAPT}
     cam, rgb, rad, st = _render_gpu(rt, sd, ro)
     assert (cam.image_width, cam.image_height) == (200, 200)
