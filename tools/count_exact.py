@@ -18,7 +18,7 @@ def main():
     if len(sys.argv) > 1:
         cfgs = [c for c in cfgs if c[0] in sys.argv[1:]]
     for scene, width, spp, depth, trav in cfgs:
-        cfg, extra = SCENES[scene]
+        cfg, extra, _ = SCENES[scene]
         cam = rt.create_camera_from_scene_data(rt.generate_scene_data(cfg), {
             "width": width, "samples": spp, "depth": depth, "aTolerance": 0, "traversal": trav, **extra})
         buf = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.uint8, device="cuda")

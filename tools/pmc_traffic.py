@@ -53,6 +53,7 @@ for n, args in enumerate(cfgs, 1):
         "hbm_bytes_per_launch_raw": (f_kib + w_kib) * 1024.0,
         "accum_kernel": {"fetch_size_kib": fetch.get("pt_accum_kernel"), "write_size_kib": write.get("pt_accum_kernel")},
         "bench_args": args,
+        "build_id": line.get("build_id"),
     }
     data[key] = entry
     print(key, json.dumps(entry))

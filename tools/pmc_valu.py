@@ -104,6 +104,7 @@ for n, args in enumerate(cfgs, 1):
                 for k, v in c.items() if k.startswith("SQ_INSTS_VALU_")},
         "counters": {k: v for k, v in sorted(c.items())},
         "bench_args": args,
+        "build_id": line.get("build_id"),
     }
     data[key] = entry
     print(key, json.dumps({k: v for k, v in entry.items() if k != "counters"}))

@@ -27,7 +27,7 @@ def main():
     if len(sys.argv) > 1:
         cfgs = [c for c in cfgs if c[0] in sys.argv[1:]]
     for scene, width, spp, depth, prec, trav in cfgs:
-        cfg, extra = SCENES[scene]
+        cfg, extra, _ = SCENES[scene]
         sd = rt.generate_scene_data(cfg)
         cam = rt.create_camera_from_scene_data(sd, {"width": width, "samples": spp, "depth": depth, "aTolerance": 0,
                                                     "precision": prec, "traversal": trav, **extra})

@@ -21,7 +21,7 @@ def main():
     extra = {"cornell": {"width": 800, "samples": 256, "depth": 16},
              "spheres": {"width": 800, "samples": 64, "depth": 8},
              "rain": {"width": 1920, "samples": 512, "depth": 16}}[scene]
-    cfg, ex = SCENES[scene]
+    cfg, ex, _ = SCENES[scene]
     cam = rt.create_camera_from_scene_data(rt.generate_scene_data(cfg), {**extra, **ex, "aTolerance": 0})
     H, W = cam.image_height, cam.image_width
     frame = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")

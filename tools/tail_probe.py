@@ -17,7 +17,7 @@ from bench import SCENES  # noqa: E402
 RO = {"cornell": {"width": 800, "samples": 256, "depth": 16}, "spheres": {"width": 800, "samples": 64, "depth": 8},
       "rain": {"width": 1920, "samples": 512, "depth": 16}}
 scene = sys.argv[1]
-cfg, ex = SCENES[scene]
+cfg, ex, _ = SCENES[scene]
 sd = rt.generate_scene_data(cfg)
 cam = rt.create_camera_from_scene_data(sd, {**RO[scene], **ex, "aTolerance": 0})
 H, W = cam.image_height, cam.image_width
