@@ -1342,25 +1342,49 @@ __device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, c
 
 __device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_memtime(); }
 
-// Diagnostic section timer (INSTR == 2): wave-cycles per path-loop section.
+// Diagnostic section timer (INSTR == 2), wave view: every psec() ends the
+// wave's current section - whichever of its lanes execute it - and charges the
+// wave-cycles since the previous psec() of ANY lane to it, together with the
+// active lanes at that point. The wave's clock and sums live in one LDS slot per
+// wave, updated by the first active lane, so time spent in code that only some
+// lanes run is attributed once, to that code.
+// Slot words: [0] last stamp, [1] start stamp, [2 + k] cycles of section k
+// (k = PR_TRIPS: loop trips), [2 + PR_WORDS + k] active lanes, [2 + 2 PR_WORDS + k] executions.
+constexpr int kProfSlot = 2 + 3 * PR_WORDS;
+constexpr int kProfWaves = 16;  // >= waves per workgroup of either kernel
 struct Prof {
-    unsigned long long secs[PR_WORDS];
-    uint32_t lanes[PR_LOOP], execs[PR_LOOP];  // active lanes / wave executions per section (first active lane)
-    unsigned long long tt, tl;
+    unsigned long long* w;  // this wave's LDS slot
 };
+template <bool PROF>
+__device__ __forceinline__ void prof_init(Prof& pf, unsigned long long* lds, int lane) {
+    if (PROF) {
+        pf.w = lds + (threadIdx.x >> 6) * kProfSlot;
+        if (lane == 0) {
+            for (int k = 0; k < kProfSlot; ++k) pf.w[k] = 0ull;
+            const unsigned long long n = __builtin_amdgcn_s_memtime();
+            pf.w[0] = n;
+            pf.w[1] = n;
+        }
+    }
+}
 template <bool PROF>
 __device__ __forceinline__ void psec(Prof& pf, int k) {
     if (PROF) {
-        const unsigned long long n = clk();
-        pf.secs[k] += n - pf.tt;
-        pf.tt = n;
-        if (k < PR_LOOP) {
-            const unsigned long long m = __ballot(1);
-            if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) {
-                pf.lanes[k] += (uint32_t)__popcll(m);
-                pf.execs[k] += 1u;
-            }
+        const unsigned long long m = __ballot(1);
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) {
+            const unsigned long long n = __builtin_amdgcn_s_memtime();
+            pf.w[2 + k] += n - pf.w[0];
+            pf.w[0] = n;
+            pf.w[2 + PR_WORDS + k] += (unsigned long long)__popcll(m);
+            pf.w[2 + 2 * PR_WORDS + k] += 1ull;
         }
+    }
+}
+template <bool PROF>
+__device__ __forceinline__ void prof_trip(Prof& pf) {
+    if (PROF) {
+        const unsigned long long m = __ballot(1);
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) pf.w[2 + PR_TRIPS] += 1ull;
     }
 }
 
@@ -1643,17 +1667,14 @@ __device__ __forceinline__ void publish_counters(const RenderOut& out, const uin
     }
     if (PROF) {
         psec<PROF>(pf, PR_TILE);
-        // s_memtime values are wave-uniform: lane 0 publishes the wave's totals
-#pragma unroll
-        for (int k = 0; k < PR_WORDS; ++k)
-            if (lane == 0) atomicAdd(&out.counters[CT_WORDS + k], pf.secs[k]);
-#pragma unroll
-        for (int k = 0; k < PR_LOOP; ++k) {
-            const unsigned long long l = wave_sum((unsigned long long)pf.lanes[k]);
-            const unsigned long long e = wave_sum((unsigned long long)pf.execs[k]);
-            if (lane == 0) {
-                atomicAdd(&out.counters[CT_WORDS + PR_WORDS + k], l);
-                atomicAdd(&out.counters[CT_WORDS + PR_WORDS + PR_LOOP + k], e);
+        // lane 0 publishes the wave's totals from its LDS slot; PR_LOOP = the wave's lifetime
+        if (lane == 0) {
+            const unsigned long long life = __builtin_amdgcn_s_memtime() - pf.w[1];
+            for (int k = 0; k < PR_WORDS; ++k)
+                atomicAdd(&out.counters[CT_WORDS + k], k == PR_LOOP ? life : pf.w[2 + k]);
+            for (int k = 0; k < PR_LOOP; ++k) {
+                atomicAdd(&out.counters[CT_WORDS + PR_WORDS + k], pf.w[2 + PR_WORDS + k]);
+                atomicAdd(&out.counters[CT_WORDS + PR_WORDS + PR_LOOP + k], pf.w[2 + 2 * PR_WORDS + k]);
             }
         }
     }
@@ -1715,14 +1736,9 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
     }
     PixStats st;
     unsigned long long st_err = 0;
+    __shared__ unsigned long long prof_lds[PROF ? kProfWaves * kProfSlot : 1];
     Prof pf;
-    if (PROF) {
-#pragma unroll
-        for (int k = 0; k < PR_WORDS; ++k) pf.secs[k] = 0;
-#pragma unroll
-        for (int k = 0; k < PR_LOOP; ++k) pf.lanes[k] = pf.execs[k] = 0u;
-        pf.tt = clk();
-    }
+    prof_init<PROF>(pf, prof_lds, lane);
 
     while (true) {
         unsigned int tile = 0;
@@ -1748,7 +1764,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
         psec<PROF>(pf, PR_TILE);
         while (active) {
             const RtCamera& C = cam_opaque();
-            if (PROF) { pf.tl = pf.tt; pf.secs[PR_TRIPS]++; }
+            prof_trip<PROF>(pf);
             if (new_path) {
                 path_begin<Real, EMIT>(C, P, pixel_center<Real>(C, i, j), pix, (uint32_t)n);
                 new_path = false;
@@ -1775,7 +1791,6 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
                 else new_path = true;
                 psec<PROF>(pf, PR_ACC);
             }
-            if (PROF) pf.secs[PR_LOOP] += clk() - pf.tl;
         }
         if (valid_px) finish_pixel(C, out, out.packed ? tile * kWave + (uint32_t)lane : pix, color, n, bsum, bmin, bmax, st);
     }
@@ -1857,14 +1872,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
         for (int k = 0; k < CT_WORDS; ++k) cnt[k] = 0;
     }
     unsigned long long st_err = 0;
+    __shared__ unsigned long long prof_lds[PROF ? kProfWaves * kProfSlot : 1];
     Prof pf;
-    if (PROF) {
-#pragma unroll
-        for (int k = 0; k < PR_WORDS; ++k) pf.secs[k] = 0;
-#pragma unroll
-        for (int k = 0; k < PR_LOOP; ++k) pf.lanes[k] = pf.execs[k] = 0u;
-        pf.tt = clk();
-    }
+    prof_init<PROF>(pf, prof_lds, lane);
 
     int pool_next = 0, pool_end = 0;  // wave-uniform
     bool exhausted = false;           // wave-uniform
@@ -1996,7 +2006,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
         } else if (slot >= 0) {
             const RtCamera& C = cam_opaque();
-            if (PROF) { pf.tl = pf.tt; pf.secs[PR_TRIPS]++; }
+            prof_trip<PROF>(pf);
             if (new_path) {
                 path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)s);
                 new_path = false;
@@ -2011,7 +2021,6 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 finish_sample(c);
                 psec<PROF>(pf, PR_ACC);
             }
-            if (PROF) pf.secs[PR_LOOP] += clk() - pf.tl;
         }
     }
     PixStats st;

@@ -40,13 +40,14 @@ def main():
         wall = time.perf_counter() - t0
         _, sec = cam.render_device(rgb_ptr=buf.data_ptr(), synchronize=True, count_work="profile")
         parts = {k: v for k, v in sec.items() if k not in ("loop", "trips") and not k.startswith(("lanes_", "execs_"))}
+        life = sec["loop"]  # summed wave lifetimes (wave-view profiler: sections sum to it)
         lanes = {k[6:]: round(v / max(sec["execs_" + k[6:]], 1), 1) for k, v in sec.items() if k.startswith("lanes_")}
         execs = {k[6:]: round(v * 64 / (W * H * spp), 3) for k, v in sec.items() if k.startswith("execs_")}
         tot = sum(parts.values())
         line = {"cfg": f"{scene} {W}x{H} spp{spp} d{depth} {prec} {trav}", "wall_ms": round(wall * 1e3, 2),
                 "trips_per_sample": round(sec["trips"] * 64 / (W * H * spp), 3),
                 "share": {k: round(v / tot, 4) for k, v in parts.items()},
-                "loop_vs_sum": round(sec["loop"] / max(tot - parts["tile"], 1), 4),
+                "sections_vs_lifetime": round(tot / max(life, 1), 4),
                 "active_lanes_per_exec": lanes, "wave_execs_per_64_samples": execs}
         print(json.dumps(line), flush=True)
 
