@@ -1813,9 +1813,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
 // chunks halve from phase to phase, so the launch ends on 1-sample items.
 constexpr int kMaxPhases = 8;
 struct SampleBuf {
-    float4* rec;    // [sample - fold][slot] {r, g, b, bounces (int bits)}
-    float4* pre;    // [slot][2]: the folded prefix {r, g, b, bounce sum}, {bounce min, max} (int bits)
-    int32_t fold;   // samples [0, fold) of a pixel form one item summed in registers (phase 0), 0 = none
+    float4* rec;    // [sample][slot] {r, g, b, bounces (int bits)}
     int32_t slots;  // pixel slots in this pass = pass_tiles * 64
     int32_t tile0;  // first of this pass's tiles (index among this launch's tiles)
     int32_t pool;   // items a wave takes from the global counter at a time (multiple of 64)
@@ -1889,45 +1887,6 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     constexpr bool RS = RT_RESUME && TRAV == TRAV_FAST && INSTR == 0;
     FastWalk<Real> W;
     bool walking = false;
-    // folded prefix item (phase 0): PixelStats.add in registers, in sample order
-    V3 facc = v3(0, 0, 0);
-    int fb = 0, fbmin = 0x7fffffff, fbmax = 0;
-
-    // the sample's radiance and bounce count: into the folded prefix (written as
-    // one record when the item ends) or to its record; then next sample or idle
-    auto finish_sample = [&](V3 c) {
-        if (s < sb.fold) {
-            facc = add(facc, c);
-            fb += P.bounces;
-            fbmin = min(fbmin, P.bounces);
-            fbmax = max(fbmax, P.bounces);
-            if (s + 1 == s_end) {
-                float4 a, b;
-                a.x = facc.x;
-                a.y = facc.y;
-                a.z = facc.z;
-                a.w = __int_as_float(fb);
-                b.x = __int_as_float(fbmin);
-                b.y = __int_as_float(fbmax);
-                b.z = 0.0f;
-                b.w = 0.0f;
-                sb.pre[(size_t)slot * 2] = a;
-                sb.pre[(size_t)slot * 2 + 1] = b;
-            }
-        } else {
-            float4 r;
-            r.x = c.x;
-            r.y = c.y;
-            r.z = c.z;
-            r.w = __int_as_float(P.bounces);
-#ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
-            sb.rec[(size_t)(s - sb.fold) * sb.slots + slot] = r;
-#endif
-        }
-        ++s;
-        if (s < s_end) new_path = true;
-        else slot = -1;
-    };
 
     while (true) {
         // hand out items to idle lanes (wave-uniform control flow); waits until
@@ -1966,10 +1925,6 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                         pix = (uint32_t)j * (uint32_t)C0.width + (uint32_t)i;
                         pc = pixel_center<Real>(cam_opaque(), i, j);
                         new_path = true;
-                        facc = v3(0, 0, 0);
-                        fb = 0;
-                        fbmin = 0x7fffffff;
-                        fbmax = 0;
                     }
                 }
                 pool_next += take;
@@ -1981,6 +1936,18 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             continue;
         }
         if constexpr (RS) {
+            // the sample's radiance and bounce count to its record; next sample or idle
+            auto finish_sample = [&](V3 c) {
+                float4 r;
+                r.x = c.x;
+                r.y = c.y;
+                r.z = c.z;
+                r.w = __int_as_float(P.bounces);
+                sb.rec[(size_t)s * sb.slots + slot] = r;
+                ++s;
+                if (s < s_end) new_path = true;
+                else slot = -1;
+            };
             const RtCamera& C = cam_opaque();
             // lanes between rays: start a path if needed, then the level's depth
             // cut-off / roulette, and the walk of its ray
@@ -2014,11 +1981,21 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
             V3 c;
             if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(S, C, P, stk, stkt, cnt, st_err, pf, c)) {
+                float4 r;
+                r.x = c.x;
+                r.y = c.y;
+                r.z = c.z;
+                r.w = __int_as_float(P.bounces);
+#ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
+                sb.rec[(size_t)s * sb.slots + slot] = r;
+#endif
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;
                     cnt[CT_BOUNCES] += (uint32_t)P.bounces;
                 }
-                finish_sample(c);
+                ++s;
+                if (s < s_end) new_path = true;
+                else slot = -1;
                 psec<PROF>(pf, PR_ACC);
             }
         }

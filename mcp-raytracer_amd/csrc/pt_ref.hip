@@ -69,23 +69,14 @@ __global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg
             unsigned long long bsum = 0;
             int bmin = 0x7fffffff, bmax = 0;
             const int n = C.n_samples;
-            int k = 0;
-            if (sb.fold > 0) {  // the folded prefix: samples [0, fold) already summed in order
-                const float4 a = sb.pre[(size_t)slot * 2], b = sb.pre[(size_t)slot * 2 + 1];
-                color = v3(a.x, a.y, a.z);
-                bsum = (unsigned long long)__float_as_int(a.w);
-                bmin = __float_as_int(b.x);
-                bmax = __float_as_int(b.y);
-                k = sb.fold;
-            }
-            // records are [sample - fold][slot] (coalesced across the wave); RT_ACC_UNROLL loads in flight
-            const size_t stride = (size_t)sb.slots;
+            // records are [sample][slot] (coalesced across the wave); RT_ACC_UNROLL loads in flight
             const float4* rec = sb.rec + slot;
-            const int f0 = sb.fold;
+            const size_t stride = (size_t)sb.slots;
+            int k = 0;
             for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
                 float4 r[RT_ACC_UNROLL];
 #pragma unroll
-                for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = rec[(size_t)(k - f0 + m) * stride];
+                for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = rec[(size_t)(k + m) * stride];
 #pragma unroll
                 for (int m = 0; m < RT_ACC_UNROLL; ++m) {
                     color = add(color, v3(r[m].x, r[m].y, r[m].z));
@@ -96,7 +87,7 @@ __global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg
                 }
             }
             for (; k < n; ++k) {
-                const float4 r = rec[(size_t)(k - f0) * stride];
+                const float4 r = rec[(size_t)k * stride];
                 color = add(color, v3(r.x, r.y, r.z));
                 const int b = __float_as_int(r.w);
                 bsum += (unsigned long long)b;

@@ -42,10 +42,6 @@ int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return (e && e[0]) ? std::max(1, std::atoi(e)) : dflt;
 }
-int env_int0(const char* name, int dflt) {  // allows 0
-    const char* e = std::getenv(name);
-    return (e && e[0]) ? std::max(0, std::atoi(e)) : dflt;
-}
 
 int set_error(int code, const std::string& msg) {
     g_error = msg;
@@ -312,33 +308,12 @@ struct rt_camera {
             ev_accum = false;
             return;
         }
-        // samples per resident lane of this launch
-        const double spl = (double)mine * kWave * (double)C.n_samples / ((double)cus * kBlockChunk);
-        // Folded prefix (phase 0): samples [0, fold) of a pixel are one item whose
-        // lane sums them in order in registers and writes one 32-byte prefix record,
-        // instead of `fold` 16-byte sample records. An item is the critical path of
-        // its pixel, so fold <= spl / 4 (pow2 floor) keeps the launch balanced, and
-        // at most half of the samples: the guided phases after it absorb the tail.
-        int fold = 0;
-        {
-            const int want = env_int0("RT_AMD_FOLD", -1);
-            if (want >= 0) {
-                fold = std::min(want, C.n_samples);
-            } else {
-                const double cap = std::min((double)C.n_samples / 2.0, spl / 4.0);
-                int f = 1;
-                while (f * 2 <= cap) f *= 2;
-                fold = f >= 8 ? f : 0;
-            }
-        }
         // chunked kernel: passes over at most sbuf_budget bytes of per-sample records
-        const size_t rec_per_tile = (size_t)kWave * ((size_t)(C.n_samples - fold) + 2) * sizeof(float4);
+        const size_t rec_per_tile = (size_t)kWave * (size_t)C.n_samples * sizeof(float4);
         const long pass_tiles = std::max<long>(1, std::min<long>(mine, (long)(sbuf_budget() / rec_per_tile)));
         ensure_sbuf((size_t)pass_tiles * rec_per_tile);
         SampleBuf sb{};
         sb.rec = d_sbuf;
-        sb.pre = d_sbuf + (size_t)pass_tiles * kWave * (size_t)(C.n_samples - fold);
-        sb.fold = fold;
 
         // guided schedule: half of the remaining samples per phase, chunks halving.
         // First-phase chunk from the samples per resident lane: an item is the
@@ -349,6 +324,7 @@ struct rt_camera {
         {
             // BVH scenes have heavy-tailed per-ray cost (grazing rays): spl / 16; brute-force
             // scenes test every primitive per ray (bounded cost): spl / 8
+            const double spl = (double)mine * kWave * (double)C.n_samples / ((double)cus * kBlockChunk);
             // items a wave takes per global atomic: two tile-chunks for large brute-force
             // launches (bounded per-ray cost: fewer atomics, Cornell 800^2 spp256 +2 %),
             // one otherwise (BVH scenes' heavy-tailed rays: wider takes cost spheres-500
@@ -357,16 +333,12 @@ struct rt_camera {
             const double per = v.trav == TRAV_BRUTE ? 8.0 : 16.0;
             int c_auto = 1;
             while (c_auto * 2 <= 32 && c_auto * 2 * per <= spl) c_auto *= 2;  // pow2 floor of spl / per, in [1, 32]
-            int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, (C.n_samples - fold) / 2)), np = 0;
-            if (fold > 0) {  // phase 0: the folded prefix, one item per pixel
-                sb.s0[np] = 0; sb.chunk[np] = fold; sb.nch[np] = 1; ++np;
-                s0 = fold;
-            }
-            if (!env_flag("RT_AMD_GUIDED", true) && s0 < C.n_samples) {  // uniform chunks (A/B)
-                c = std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples - s0);
-                const int full = (C.n_samples - s0) / c;
-                sb.s0[np] = s0; sb.chunk[np] = c; sb.nch[np] = full; ++np;
-                s0 += full * c;
+            int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2)), np = 0;
+            if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
+                c = std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples);
+                const int full = C.n_samples / c;
+                sb.s0[np] = 0; sb.chunk[np] = c; sb.nch[np] = full; ++np;
+                s0 = full * c;
             }
             while (s0 < C.n_samples) {
                 const int rem = C.n_samples - s0;
