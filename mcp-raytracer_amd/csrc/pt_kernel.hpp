@@ -1813,7 +1813,8 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
 // chunks halve from phase to phase, so the launch ends on 1-sample items.
 constexpr int kMaxPhases = 8;
 struct SampleBuf {
-    float4* rec;    // [sample][slot] {r, g, b, bounces (int bits)}
+    float4* rec;    // record of (sample s, pixel slot) at s * stride_s + slot * stride_slot: {r, g, b, bounces (int bits)}
+    int64_t stride_s, stride_slot;  // sample-major ([sample][slot]) or slot-major ([slot][sample])
     int32_t slots;  // pixel slots in this pass = pass_tiles * 64
     int32_t tile0;  // first of this pass's tiles (index among this launch's tiles)
     int32_t pool;   // items a wave takes from the global counter at a time (multiple of 64)
@@ -1943,7 +1944,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 r.y = c.y;
                 r.z = c.z;
                 r.w = __int_as_float(P.bounces);
-                sb.rec[(size_t)s * sb.slots + slot] = r;
+                sb.rec[(size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot] = r;
                 ++s;
                 if (s < s_end) new_path = true;
                 else slot = -1;
@@ -1987,7 +1988,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 r.z = c.z;
                 r.w = __int_as_float(P.bounces);
 #ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
-                sb.rec[(size_t)s * sb.slots + slot] = r;
+                sb.rec[(size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot] = r;
 #endif
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;

@@ -69,9 +69,10 @@ __global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg
             unsigned long long bsum = 0;
             int bmin = 0x7fffffff, bmax = 0;
             const int n = C.n_samples;
-            // records are [sample][slot] (coalesced across the wave); RT_ACC_UNROLL loads in flight
-            const float4* rec = sb.rec + slot;
-            const size_t stride = (size_t)sb.slots;
+            // RT_ACC_UNROLL loads in flight; sample-major records are coalesced across the
+            // wave, slot-major ones are one contiguous run per lane
+            const float4* rec = sb.rec + (size_t)slot * sb.stride_slot;
+            const size_t stride = (size_t)sb.stride_s;
             int k = 0;
             for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
                 float4 r[RT_ACC_UNROLL];

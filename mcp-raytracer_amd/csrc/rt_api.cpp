@@ -370,6 +370,14 @@ struct rt_camera {
             const long nt = std::min(pass_tiles, mine - t0);
             sb.tile0 = (int32_t)t0;
             sb.slots = (int32_t)(nt * kWave);
+            // record layout: sample-major (default) or slot-major (RT_AMD_REC_SLOT_MAJOR=1, A/B)
+            if (env_flag("RT_AMD_REC_SLOT_MAJOR", false)) {
+                sb.stride_s = 1;
+                sb.stride_slot = C.n_samples;
+            } else {
+                sb.stride_s = sb.slots;
+                sb.stride_slot = 1;
+            }
             long items = 0;
             for (int p = 0; p < sb.n_phases; ++p) {
                 sb.item_base[p] = (int32_t)items;
