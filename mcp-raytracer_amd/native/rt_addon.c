@@ -189,6 +189,45 @@ static napi_value RenderRegion(napi_env env, napi_callback_info info) {
     return out;
 }
 
+static void finalize_free(napi_env env, void* data, void* hint) {
+    (void)env;
+    (void)hint;
+    rt_free(data);
+}
+
+/* encodePng(pixels: Uint8ClampedArray | Uint8Array (width*height*3), width, height) -> Buffer
+ * (rt_encode_png: 8-bit RGB PNG): the step generateImageBuffer hands to sharp
+ * (src/raytracer.ts:101-110). */
+static napi_value EncodePng(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bool is_ta = false;
+    if (argc < 3 || napi_is_typedarray(env, argv[0], &is_ta) != napi_ok || !is_ta) {
+        napi_throw_type_error(env, NULL, "encodePng(pixels: Uint8ClampedArray, width, height)");
+        return NULL;
+    }
+    napi_typedarray_type tt;
+    size_t len = 0, off = 0;
+    void* data = NULL;
+    napi_value ab;
+    CHECK_NAPI(env, napi_get_typedarray_info(env, argv[0], &tt, &len, &data, &ab, &off));
+    int32_t w = 0, h = 0;
+    CHECK_NAPI(env, napi_get_value_int32(env, argv[1], &w));
+    CHECK_NAPI(env, napi_get_value_int32(env, argv[2], &h));
+    if ((tt != napi_uint8_clamped_array && tt != napi_uint8_array) || w <= 0 || h <= 0 ||
+        len < (size_t)w * (size_t)h * 3u) {
+        napi_throw_range_error(env, NULL, "pixels must hold width*height*3 bytes");
+        return NULL;
+    }
+    uint8_t* png = NULL;
+    size_t n = 0;
+    if (rt_encode_png((const uint8_t*)data, w, h, 6, &png, &n)) return throw_rt(env);
+    napi_value buf;
+    CHECK_NAPI(env, napi_create_external_buffer(env, n, png, finalize_free, NULL, &buf));
+    return buf;
+}
+
 static napi_value Version(napi_env env, napi_callback_info info) {
     (void)info;
     napi_value v;
@@ -202,6 +241,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"createCamera", NULL, CreateCamera, NULL, NULL, NULL, napi_default, NULL},
         {"cameraInfo", NULL, CameraInfo, NULL, NULL, NULL, napi_default, NULL},
         {"renderRegion", NULL, RenderRegion, NULL, NULL, NULL, napi_default, NULL},
+        {"encodePng", NULL, EncodePng, NULL, NULL, NULL, napi_default, NULL},
         {"version", NULL, Version, NULL, NULL, NULL, napi_default, NULL},
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);

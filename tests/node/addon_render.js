@@ -27,7 +27,15 @@ if (mode === 'info') {
   const s1 = addon.renderRegion(cam, pixels, { x: 0, y: 0, width: info.imageWidth, height: half });
   const s2 = addon.renderRegion(cam, pixels, { x: 0, y: half, width: info.imageWidth, height: info.imageHeight - half });
   fs.writeFileSync(process.argv[4], Buffer.from(shared));
+  fs.writeFileSync(process.argv[4] + '.png', addon.encodePng(pixels, info.imageWidth, info.imageHeight));
   console.log(JSON.stringify({ width: info.imageWidth, height: info.imageHeight, stats: [s1, s2] }));
+} else if (mode === 'png') {
+  // host-only: encodePng of a synthetic frame (no GPU)
+  const w = 5, h = 3;
+  const px = new Uint8ClampedArray(w * h * 3);
+  for (let k = 0; k < px.length; ++k) px[k] = (k * 7) % 251;
+  fs.writeFileSync(process.argv[4], addon.encodePng(px, w, h));
+  console.log(JSON.stringify({ width: w, height: h }));
 } else if (mode === 'errors') {
   const msgs = [];
   const bad = JSON.parse(sceneJson);

@@ -45,6 +45,16 @@ def test_addon_throws_reference_errors(addon):
     assert "camera" in msgs[2]
 
 
+def test_addon_encode_png(addon, tmp_path):
+    """encodePng (rt_encode_png) from Node: the PNG decodes to the frame's bytes."""
+    from raytracer_amd.png import decode_png_rgb
+    out = tmp_path / "f.png"
+    res = _node(addon, "png", out)
+    w, h, px = decode_png_rgb(out.read_bytes())
+    assert (w, h) == (res["width"], res["height"]) == (5, 3)
+    assert px == bytes((k * 7) % 251 for k in range(5 * 3 * 3))
+
+
 @pytest.mark.gpu
 def test_addon_render_matches_python_binding(rt, addon, gpu, tmp_path):
     """Two renderRegion calls into one SharedArrayBuffer (the worker split of
@@ -58,5 +68,7 @@ def test_addon_render_matches_python_binding(rt, addon, gpu, tmp_path):
     ref = np.zeros((H, W, 3), np.uint8)
     st = cam.render(ref)
     assert np.array_equal(got, ref)
+    from raytracer_amd.png import decode_png_rgb
+    assert decode_png_rgb(Path(str(out_bin) + ".png").read_bytes()) == (W, H, ref.tobytes())
     assert sum(s["pixels"] for s in res["stats"]) == st.pixels
     assert sum(s["samples"]["total"] for s in res["stats"]) == st.samples["total"]
