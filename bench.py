@@ -153,6 +153,8 @@ def parse_args(argv):
     ap.add_argument("--count-sub", type=int, default=0,
                     help="tile subsample of the work-counting launch (0 = auto: 16 above 1000 objects)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--check", action="store_true",
+                    help="rank 0 compares the assembled frame with a single-launch render of the whole image")
     ap.add_argument("--stub", action="store_true",
                     help="CPU rehearsal of the launcher and the gather (gloo, no GPU, no render: tests only)")
     return ap.parse_args(argv)
@@ -230,11 +232,16 @@ def main(argv=None):
 
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one GPU per rank; more ranks than devices (a CPU-backend rehearsal on one GPU) share them
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     world = 1
     if world_env > 1:
-        dist.init_process_group(args.backend, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
         world = dist.get_world_size()  # the ranks RCCL actually connected
     from raytracer_amd import _build
 
@@ -319,10 +326,20 @@ def main(argv=None):
     accum_ms = sum(b for _, b in kt) / len(kt)
     kernel_name = "pt_chunk_kernel" if accum_ms > 0 else "pt_render_kernel"
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
+
+    frame_check = None
+    if args.check:
+        step()  # a fresh assembled frame
+        torch.cuda.synchronize()
+        if rank == 0:
+            single = torch.zeros_like(frame)
+            cam.render_device(rgb_ptr=single.data_ptr(), stream=sptr, synchronize=True)
+            frame_check = bool(torch.equal(single, frame))
+            log(f"frame check (assembled == single launch): {frame_check}")
 
     if rank == 0:
         samples_per_step = W * H * args.spp
@@ -353,6 +370,7 @@ def main(argv=None):
                        "parallelism": f"8x8-tile interleave x{world}" +
                                       (" + RCCL gather of tile-packed slabs to rank 0" if world > 1 else "")},
             "build_id": rt.build_id(),
+            **({"frame_check": frame_check} if args.check else {}),
             "roofline": rl,
             "cpu_baseline": cpu,
         }

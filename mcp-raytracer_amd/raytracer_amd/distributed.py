@@ -63,6 +63,15 @@ def gather_slabs(slab, world: int, out=None, group=None):
 
     if world == 1:
         return slab.unsqueeze(0)
+    if slab.is_cuda and dist.get_backend(group) == "gloo":
+        # CPU-backend rehearsal (several ranks on one GPU): gloo gathers host tensors only
+        g = gather_slabs(slab.cpu(), world, group=group)
+        if g is None:
+            return None
+        if out is None:
+            return g.to(slab.device)
+        out.copy_(g)
+        return out
     rank = dist.get_rank(group)
     if rank == 0:
         if out is None:

@@ -671,3 +671,22 @@ def test_generate_image_buffer_png_pixels_equal_render(rt, gpu):
     cam.render(rgb)
     w, h, px = decode_png_rgb(png)
     assert (w, h) == (32, 32) and px == rgb.tobytes()
+
+
+def test_bench_two_ranks_one_gpu_assemble_the_frame(gpu):
+    """bench.py's multi-GPU path end to end on one device: 2 ranks (launched by
+    bench.py --gpus 2 itself) render their tile-packed shares, gather them over a
+    CPU backend and rank 0 unpacks them; the frame equals one single-launch render."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "2",
+                        "--warmup", "1", "--no-cpu", "--no-count", "--check", "--width", "200", "--spp", "16"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "frame_check")})
+    assert line["n_gpus"] == 2 and line["frame_check"] is True
