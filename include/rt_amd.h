@@ -160,6 +160,10 @@ int rt_camera_export(const rt_camera* cam, void* nodes, void* prims, void* mater
 int rt_debug_world_hit(rt_camera* cam, int32_t traversal, int32_t n, const float* orig, const float* dir,
                        double* out);
 
+/* The device's Math.cos(phi), Math.sin(phi) (phi = 2 PI xi, the cosine-PDF angle)
+ * and Math.pow(xi, 5) (Schlick) for xi = u[k] / 2^32: out = host double[3*n]. */
+int rt_debug_math(int32_t n, const uint32_t* u, double* out);
+
 /* The path RNG stream (seeded Math.random replacement), host evaluation. */
 int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out);
 

@@ -155,6 +155,27 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
     }
 }
 
+// The device's Math.cos / Math.sin of the cosine-PDF angle and Schlick's
+// Math.pow(x, 5), with the path code's own expressions (pt_kernel.hpp path_post,
+// dielectric_dir): phi = 2 * PI * xi, xi = u * 2^-32.
+__global__ void math_probe_kernel(int n, const uint32_t* u, double* out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double xi = (double)u[k] * (1.0 / 4294967296.0);
+    const double phi = 2.0 * K<double>::PI * xi;
+    double sn, cs;
+    m_sincos(phi, sn, cs);
+    out[3 * k] = cs;
+    out[3 * k + 1] = sn;
+    out[3 * k + 2] = pow5(xi);
+}
+
+hipError_t launch_math_probe(int n, const uint32_t* u, double* out, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n, u, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float* orig, const float* dir,
                                 double* out, hipStream_t stream) {
     const int grid = (n + kBlock - 1) / kBlock;

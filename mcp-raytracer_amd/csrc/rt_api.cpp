@@ -673,6 +673,27 @@ int rt_debug_world_hit(rt_camera* cam, int32_t traversal, int32_t n, const float
     }
 }
 
+int rt_debug_math(int32_t n, const uint32_t* u, double* out) {
+    if (n < 0 || (n > 0 && (!u || !out))) return set_error(RT_ERR_INVALID, "bad arguments");
+    uint32_t* d_u = nullptr;
+    double* d_out = nullptr;
+    try {
+        if (n == 0) return RT_OK;
+        hip_check(hipMalloc(&d_u, (size_t)n * sizeof(uint32_t)), "hipMalloc");
+        hip_check(hipMalloc(&d_out, (size_t)n * 3 * sizeof(double)), "hipMalloc");
+        hip_check(hipMemcpy(d_u, u, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
+        hip_check(launch_math_probe(n, d_u, d_out, nullptr), "math_probe_kernel");
+        hip_check(hipMemcpy(out, d_out, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+        (void)hipFree(d_u);
+        (void)hipFree(d_out);
+        return RT_OK;
+    } catch (const std::exception& e) {
+        if (d_u) (void)hipFree(d_u);
+        if (d_out) (void)hipFree(d_out);
+        return set_error(RT_ERR_DEVICE, e.what());
+    }
+}
+
 int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out) {
     if (n < 0 || (n > 0 && !out)) return set_error(RT_ERR_INVALID, "bad arguments");
     uint64_t s = splitmix64((((uint64_t)pixel << 32) | sample) ^ splitmix64(seed));

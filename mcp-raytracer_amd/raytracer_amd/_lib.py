@@ -83,6 +83,7 @@ _SIGS = {
                                    C.c_void_p]),
     "rt_debug_world_hit": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_void_p]),
+    "rt_debug_math": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "rt_camera_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "rt_camera_pass_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),

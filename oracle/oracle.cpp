@@ -1200,6 +1200,19 @@ void or_reflect(const double* v, const double* n, double* out) { put(out, V(v).r
 void or_refract(const double* v, const double* n, double eta, double* out) { put(out, V(v).refract(V(n), eta)); }
 void or_unit(const double* v, double* out) { put(out, V(v).unitVector()); }
 double or_length(const double* v) { return V(v).length(); }
+// The oracle's Math.cos / Math.sin of the cosine-PDF angle phi = 2 * PI * xi,
+// xi = u / 2^32 (Vec3.randomCosineDirection, src/geometry/vec3.ts:325-337), and
+// Schlick's Math.pow(xi, 5) (src/materials/dielectric.ts:98): for the V8 fixture
+// (tests/golden/v8_math.npz, tests/test_v8_math.py).
+void or_math_probe(int n, const uint32_t* u, double* out) {
+    for (int k = 0; k < n; ++k) {
+        const double xi = (double)u[k] * (1.0 / 4294967296.0);
+        const double phi = 2 * M_PI * xi;
+        out[3 * k] = R_cos<double>(phi);
+        out[3 * k + 1] = R_sin<double>(phi);
+        out[3 * k + 2] = R_pow5(xi);
+    }
+}
 // Mixture value with fixed component values (tests/geometry/pdf.test.ts:126-156)
 double or_mixture_value(int n, const double* values, const double* weights) {
     struct VP : PDF<double> { double x; double value(const Vec3<double>&) const override { return x; } Vec3<double> generate() const override { return Vec3<double>(); } };

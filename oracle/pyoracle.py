@@ -70,6 +70,8 @@ def load():
         lib.or_mixture_value.restype = C.c_double
         lib.or_rng_stream.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p]
         lib.or_camera_info.argtypes = [C.c_char_p, C.c_char_p, D]
+        lib.or_math_probe.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+        lib.or_math_probe.restype = None
         _lib = lib
     return _lib
 
@@ -219,3 +221,11 @@ def camera_info(scene: dict, render_opts: dict | None = None):
         raise _err()
     return {"width": int(out[0]), "height": int(out[1]), "pixel00": list(out[2:5]), "du": list(out[5:8]),
             "dv": list(out[8:11]), "center": list(out[11:14])}
+
+
+def math_probe(u):
+    """The oracle's (cos(phi), sin(phi), pow(xi, 5)) for xi = u / 2^32, phi = 2 pi xi."""
+    u = np.ascontiguousarray(u, dtype=np.uint32)
+    out = np.zeros((u.size, 3), dtype=np.float64)
+    load().or_math_probe(int(u.size), u.ctypes.data, out.ctypes.data)
+    return out
