@@ -591,6 +591,39 @@ __device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi,
     return true;
 }
 
+// sphere_maybe plus, when the sphere is SURELY hit at some t > 0.001 (the exact
+// discriminant is positive and the larger root exceeds tMin under the same error
+// model), an upper bound `hi` of the t the exact test will return (+inf otherwise).
+// A surely-hit candidate's `hi` may cull the walk before its exact test runs.
+#ifndef RT_DEFER_EXACT
+#define RT_DEFER_EXACT 1
+#endif
+__device__ __forceinline__ bool sphere_maybe_hi(float4 g, const FRay& f, float thi, float& lo, float& hi) {
+    const float ox = f.o[0] - g.x, oy = f.o[1] - g.y, oz = f.o[2] - g.z;
+    const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
+    const float r = g.w;
+    const float oo = ox * ox + oy * oy + oz * oz;
+    const float disc = b * b - f.a * (oo - r * r);
+    const float tol = 4.0f * kRel * f.a * (oo + r * r) + 1e-30f;
+    if (disc < -tol) return false;
+    const float sq = __builtin_amdgcn_sqrtf(::fmaxf(disc, 0.0f) + tol) * (1.0f + kRel);
+    const float et = kRel * (__builtin_amdgcn_sqrtf(oo * f.a) + ::fabsf(b) + sq) * f.ia + 1e-30f;
+    const float hi2 = (-b + sq) * f.ia * (1.0f + kRel) + et;  // >= every root
+    if (hi2 < kTminLo) return false;
+    const float r1 = (-b - sq) * f.ia;
+    lo = r1 - ::fabsf(r1) * kRel - et;  // <= the first root; the second is larger
+    if (lo > thi) return false;
+    hi = __builtin_inff();
+    const float dm = disc - tol;  // <= the exact discriminant
+    if (dm > 0.0f) {
+        const float sql = __builtin_amdgcn_sqrtf(dm) * (1.0f - kRel);  // <= its square root
+        const float r2 = (-b + sql) * f.ia;
+        const float r2lo = r2 - ::fabsf(r2) * kRel - et;                // <= the larger root
+        if (r2lo > 0.001f * (1.0f + 1e-5f)) hi = hi2 * (1.0f + 4e-6f) + 1e-30f;
+    }
+    return true;
+}
+
 template <bool QUAD>
 __device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, float thi, float& lo) {
     const float nx = p.g3[0], ny = p.g3[1], nz = p.g3[2];
@@ -683,9 +716,33 @@ __device__ __forceinline__ float upper_f(Real t) {
 #endif
 constexpr int kTravDone = (int)0x80000000;  // no node / leaf (leaf refs are ~v, v < 2^31 - 1)
 
+// Deferred exact sphere tests (RT_DEFER_EXACT): a leaf's sphere that passes the
+// fp32 pre-filter becomes this lane's PENDING candidate instead of being tested
+// exactly on the spot - lanes reach leaves at different steps, so an in-loop
+// fp64 test ran with a handful of active lanes (spheres-100k: 14 wave-level
+// exact blocks per ray-trip for 1.0 tests per ray). A surely-hit candidate's
+// upper bound culls the walk meanwhile; a second candidate resolves the first;
+// the walk's end resolves the last, batched over the lanes finishing together.
+// Exact t and the (t, slot) minimum are unchanged.
+template <class Real, bool COUNT>
+__device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Real>& r, float& thi, Real& best_t,
+                                                int& best, int& pk, uint32_t* cnt) {
+    if (pk >= 0) {
+        if (COUNT) count_exact(cnt);
+        Real t;
+        if (sphere_t<Real>(S.prims[pk], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t) &&
+            (t < best_t || (t == best_t && pk < best))) {
+            best_t = t;
+            best = pk;
+            thi = ::fminf(thi, upper_f<Real>(t));
+        }
+        pk = -1;
+    }
+}
+
 template <class Real, bool COUNT>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
-                                          Real& best_t, int& best, uint32_t* cnt) {
+                                          Real& best_t, int& best, int& pk, uint32_t* cnt) {
     const int v = ~ref;
     const int first = v >> 3;
     const int end = first + (v & 7);
@@ -697,10 +754,22 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
         if (g.w == g.w) {  // sphere: pre-filter from the compact leaf-order record
             if (COUNT) cnt[CT_SPHERE]++;
             float lo;
+#if RT_DEFER_EXACT
+            float hi;
+            if (!sphere_maybe_hi(g, f, thi, lo, hi)) continue;
+            k = S.tprims[m];
+            resolve_pending<Real, COUNT>(S, r, thi, best_t, best, pk, cnt);  // a second candidate: settle the first
+            if (lo <= thi) {
+                pk = k;
+                thi = ::fminf(thi, hi);
+            }
+            continue;
+#else
             if (!sphere_maybe(g, f, thi, lo)) continue;
             if (COUNT) count_exact(cnt);
             k = S.tprims[m];
             cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
+#endif
         } else {
             k = S.tprims[m];
             cand = prim_candidate<Real, COUNT>(S.prims[k], ray_at_use<Real>(r), f, thi, t, cnt);
@@ -708,7 +777,7 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
         if (cand && (t < best_t || (t == best_t && k < best))) {
             best_t = t;
             best = k;
-            thi = upper_f<Real>(t);
+            thi = ::fminf(thi, upper_f<Real>(t));
         }
     }
 }
@@ -719,6 +788,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     const FRay f = make_fray(r.o, r.d);
     Real best_t = (Real)__builtin_inf();
     int best = -1;
+    int pk = -1;  // pending (deferred) exact sphere test
     float thi = __builtin_inff();
     float tn0;
     if (COUNT) cnt[CT_NODE]++;
@@ -823,7 +893,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             ref = pop();
         }
         while (leaf != kTravDone) {
-            leaf_test<Real, COUNT>(S, leaf, r, f, thi, best_t, best, cnt);
+            leaf_test<Real, COUNT>(S, leaf, r, f, thi, best_t, best, pk, cnt);
             leaf = kTravDone;
             if (ref < 0 && ref != kTravDone) {  // the walk also stopped on a leaf
                 leaf = ref;
@@ -834,13 +904,14 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
 #else
     while (ref != kTravDone) {
         if (ref < 0) {
-            leaf_test<Real, COUNT>(S, ref, r, f, thi, best_t, best, cnt);
+            leaf_test<Real, COUNT>(S, ref, r, f, thi, best_t, best, pk, cnt);
             ref = pop();
         } else {
             ref = node_step(ref);
         }
     }
 #endif
+    resolve_pending<Real, COUNT>(S, r, thi, best_t, best, pk, cnt);  // the whole wave at once
     t_hit = best_t;
     return best;
 }
@@ -861,6 +932,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
 template <class Real>
 struct FastWalk {
     int ref, leaf, sp, best;
+    int pk;  // pending (deferred) exact sphere test, resolved by fast_walk_resolve
     float thi;
     Real best_t;
 };
@@ -872,6 +944,7 @@ __device__ __forceinline__ void fast_walk_begin(const DevScene& S, V3 o, V3 d, F
     W.best = -1;
     W.thi = __builtin_inff();
     W.sp = 0;
+    W.pk = -1;
     W.leaf = kTravDone;
     float tn0;
     if (COUNT) cnt[CT_NODE]++;
@@ -987,7 +1060,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 ref = pop();
             }
             while (leaf != kTravDone) {
-                leaf_test<Real, COUNT>(S, leaf, r, f, thi, W.best_t, W.best, cnt);
+                leaf_test<Real, COUNT>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, cnt);
                 leaf = kTravDone;
                 if (ref < 0 && ref != kTravDone) {
                     leaf = ref;
@@ -1001,6 +1074,14 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             if (ref == kTravDone && leaf == kTravDone) walking = false;
         }
     }
+}
+
+// The exact test of a finished walk's pending candidate (called by the lanes whose
+// walks ended, together, before they shade).
+template <class Real, bool COUNT>
+__device__ __forceinline__ void fast_walk_resolve(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, uint32_t* cnt) {
+    const RayK<Real> r = make_ray<Real>(o, d);
+    resolve_pending<Real, COUNT>(S, r, W.thi, W.best_t, W.best, W.pk, cnt);
 }
 
 // Small scenes: test every primitive in leaf order. The answer is the same
@@ -1969,6 +2050,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             fast_walk_rounds<Real, COUNT>(S, P.o, P.d, W, walking, stk, sb.min_ready, exhausted, cnt);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)
             if (was_walking && !walking) {
+                fast_walk_resolve<Real, COUNT>(S, P.o, P.d, W, cnt);
                 V3 c;
                 if (path_post<Real, EMIT, COUNT, PROF>(S, C, P, W.best, W.best_t, cnt, st_err, pf, c)) finish_sample(c);
             }
