@@ -727,6 +727,7 @@ constexpr int kTravDone = (int)0x80000000;  // no node / leaf (leaf refs are ~v,
 template <class Real, bool COUNT>
 __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Real>& r, float& thi, Real& best_t,
                                                 int& best, int& pk, uint32_t* cnt) {
+    // (pk < 0: nothing pending)
     if (pk >= 0) {
         if (COUNT) count_exact(cnt);
         Real t;
@@ -742,7 +743,7 @@ __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Re
 
 template <class Real, bool COUNT>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
-                                          Real& best_t, int& best, int& pk, uint32_t* cnt) {
+                                          Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt) {
     const int v = ~ref;
     const int first = v >> 3;
     const int end = first + (v & 7);
@@ -758,9 +759,13 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
             float hi;
             if (!sphere_maybe_hi(g, f, thi, lo, hi)) continue;
             k = S.tprims[m];
-            resolve_pending<Real, COUNT>(S, r, thi, best_t, best, pk, cnt);  // a second candidate: settle the first
+            // a second candidate: one surely hit before the pending one's lower bound
+            // replaces it untested (t_new <= hi < plo <= t_pending); otherwise the
+            // pending one is settled first
+            if (pk >= 0 && !(hi < plo)) resolve_pending<Real, COUNT>(S, r, thi, best_t, best, pk, cnt);
             if (lo <= thi) {
                 pk = k;
+                plo = lo;
                 thi = ::fminf(thi, hi);
             }
             continue;
@@ -789,6 +794,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     Real best_t = (Real)__builtin_inf();
     int best = -1;
     int pk = -1;  // pending (deferred) exact sphere test
+    float plo = 0.0f;  // its lower bound
     float thi = __builtin_inff();
     float tn0;
     if (COUNT) cnt[CT_NODE]++;
@@ -893,7 +899,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             ref = pop();
         }
         while (leaf != kTravDone) {
-            leaf_test<Real, COUNT>(S, leaf, r, f, thi, best_t, best, pk, cnt);
+            leaf_test<Real, COUNT>(S, leaf, r, f, thi, best_t, best, pk, plo, cnt);
             leaf = kTravDone;
             if (ref < 0 && ref != kTravDone) {  // the walk also stopped on a leaf
                 leaf = ref;
@@ -904,7 +910,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
 #else
     while (ref != kTravDone) {
         if (ref < 0) {
-            leaf_test<Real, COUNT>(S, ref, r, f, thi, best_t, best, pk, cnt);
+            leaf_test<Real, COUNT>(S, ref, r, f, thi, best_t, best, pk, plo, cnt);
             ref = pop();
         } else {
             ref = node_step(ref);
@@ -932,7 +938,8 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
 template <class Real>
 struct FastWalk {
     int ref, leaf, sp, best;
-    int pk;  // pending (deferred) exact sphere test, resolved by fast_walk_resolve
+    int pk;     // pending (deferred) exact sphere test, resolved by fast_walk_resolve
+    float plo;  // its lower bound
     float thi;
     Real best_t;
 };
@@ -1060,7 +1067,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 ref = pop();
             }
             while (leaf != kTravDone) {
-                leaf_test<Real, COUNT>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, cnt);
+                leaf_test<Real, COUNT>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
                 if (ref < 0 && ref != kTravDone) {
                     leaf = ref;
