@@ -28,6 +28,7 @@ struct KernelVariant {
     bool emit;   // emission stack (a scattering material emits)
     int count;   // 0 product, 1 work counters, 2 section timing (diagnostic)
     int trav;    // TRAV_FAST / TRAV_REFERENCE / TRAV_BRUTE (resolved, never AUTO)
+    bool defer = false;  // TRAV_FAST: deferred exact sphere tests (TRAV_FAST_DEFER kernels)
 };
 
 // sb == nullptr: the sequential-pixel kernel; else the chunked kernel over sb's pass.

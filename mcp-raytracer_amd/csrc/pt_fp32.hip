@@ -20,7 +20,7 @@ template <bool EMIT, int INSTR, int TRAV>
 static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                      const SampleBuf* sb, hipStream_t stream) {
     // LDS residency levels (pt_kernel.hpp scene_prologue); never with the reference traversal
-    constexpr int L1 = TRAV == TRAV_FAST ? 1 : 0, L2 = TRAV == TRAV_REFERENCE ? 0 : 2;
+    constexpr int L1 = trav_fast(TRAV) ? 1 : 0, L2 = TRAV == TRAV_REFERENCE ? 0 : 2;
     if (g.lds_level >= 2) return go2<EMIT, INSTR, TRAV, L2>(S, reg, out, g, sb, stream);
     if (g.lds_level == 1) return go2<EMIT, INSTR, TRAV, L1>(S, reg, out, g, sb, stream);
     return go2<EMIT, INSTR, TRAV, 0>(S, reg, out, g, sb, stream);
@@ -37,7 +37,8 @@ static hipError_t go_t(const KernelVariant& v, const DevScene& S, const RtRegion
 hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
                              const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
     if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, sb, stream);
-    if (v.trav == TRAV_FAST) return go_t<TRAV_FAST>(v, S, reg, out, g, sb, stream);
+    if (v.trav == TRAV_FAST)
+        return v.defer ? go_t<TRAV_FAST_DEFER>(v, S, reg, out, g, sb, stream) : go_t<TRAV_FAST>(v, S, reg, out, g, sb, stream);
     return go_t<TRAV_REFERENCE>(v, S, reg, out, g, sb, stream);
 }
 

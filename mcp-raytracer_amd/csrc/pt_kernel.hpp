@@ -103,7 +103,9 @@ struct RenderOut {
 
 // Closest-hit strategies; all return the reference's hit bit-for-bit (see the
 // functions below). AUTO is resolved on the host.
-enum Traversal : int32_t { TRAV_FAST = 0, TRAV_REFERENCE = 1, TRAV_BRUTE = 2, TRAV_AUTO = 3 };
+enum Traversal : int32_t { TRAV_FAST = 0, TRAV_REFERENCE = 1, TRAV_BRUTE = 2, TRAV_AUTO = 3,
+                           TRAV_FAST_DEFER = 4 };  // kernel-internal: FAST with deferred exact sphere tests
+constexpr bool trav_fast(int t) { return t == TRAV_FAST || t == TRAV_FAST_DEFER; }
 constexpr int kBruteMaxPrims = 16;  // AUTO picks BRUTE up to this many primitives (nearest-first form: <= 32)
 
 // Minimum waves per SIMD the path kernel is register-allocated for
@@ -595,9 +597,6 @@ __device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi,
 // discriminant is positive and the larger root exceeds tMin under the same error
 // model), an upper bound `hi` of the t the exact test will return (+inf otherwise).
 // A surely-hit candidate's `hi` may cull the walk before its exact test runs.
-#ifndef RT_DEFER_EXACT
-#define RT_DEFER_EXACT 1
-#endif
 __device__ __forceinline__ bool sphere_maybe_hi(float4 g, const FRay& f, float thi, float& lo, float& hi) {
     const float ox = f.o[0] - g.x, oy = f.o[1] - g.y, oz = f.o[2] - g.z;
     const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
@@ -716,7 +715,7 @@ __device__ __forceinline__ float upper_f(Real t) {
 #endif
 constexpr int kTravDone = (int)0x80000000;  // no node / leaf (leaf refs are ~v, v < 2^31 - 1)
 
-// Deferred exact sphere tests (RT_DEFER_EXACT): a leaf's sphere that passes the
+// Deferred exact sphere tests (DEFER, TRAV_FAST_DEFER kernels): a leaf's sphere that passes the
 // fp32 pre-filter becomes this lane's PENDING candidate instead of being tested
 // exactly on the spot - lanes reach leaves at different steps, so an in-loop
 // fp64 test ran with a handful of active lanes (spheres-100k: 14 wave-level
@@ -741,7 +740,7 @@ __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Re
     }
 }
 
-template <class Real, bool COUNT>
+template <class Real, bool COUNT, bool DEFER>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
                                           Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt) {
     const int v = ~ref;
@@ -755,7 +754,7 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
         if (g.w == g.w) {  // sphere: pre-filter from the compact leaf-order record
             if (COUNT) cnt[CT_SPHERE]++;
             float lo;
-#if RT_DEFER_EXACT
+            if constexpr (DEFER) {
             float hi;
             if (!sphere_maybe_hi(g, f, thi, lo, hi)) continue;
             k = S.tprims[m];
@@ -769,12 +768,12 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
                 thi = ::fminf(thi, hi);
             }
             continue;
-#else
+            } else {
             if (!sphere_maybe(g, f, thi, lo)) continue;
             if (COUNT) count_exact(cnt);
             k = S.tprims[m];
             cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
-#endif
+            }
         } else {
             k = S.tprims[m];
             cand = prim_candidate<Real, COUNT>(S.prims[k], ray_at_use<Real>(r), f, thi, t, cnt);
@@ -787,7 +786,7 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
     }
 }
 
-template <class Real, bool COUNT>
+template <class Real, bool COUNT, bool DEFER>
 __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
                                                 float* stkt, uint32_t* cnt) {
     const FRay f = make_fray(r.o, r.d);
@@ -899,7 +898,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             ref = pop();
         }
         while (leaf != kTravDone) {
-            leaf_test<Real, COUNT>(S, leaf, r, f, thi, best_t, best, pk, plo, cnt);
+            leaf_test<Real, COUNT, DEFER>(S, leaf, r, f, thi, best_t, best, pk, plo, cnt);
             leaf = kTravDone;
             if (ref < 0 && ref != kTravDone) {  // the walk also stopped on a leaf
                 leaf = ref;
@@ -910,7 +909,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
 #else
     while (ref != kTravDone) {
         if (ref < 0) {
-            leaf_test<Real, COUNT>(S, ref, r, f, thi, best_t, best, pk, plo, cnt);
+            leaf_test<Real, COUNT, DEFER>(S, ref, r, f, thi, best_t, best, pk, plo, cnt);
             ref = pop();
         } else {
             ref = node_step(ref);
@@ -961,7 +960,7 @@ __device__ __forceinline__ void fast_walk_begin(const DevScene& S, V3 o, V3 d, F
 // Called by the whole wave with uniform control flow; lanes with `walking`
 // advance their walks. Returns when no lane walks, or (unless `drain`) after at
 // least one round once `min_ready` lanes of the wave are not walking.
-template <class Real, bool COUNT>
+template <class Real, bool COUNT, bool DEFER>
 __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, bool& walking,
                                                  int* stk, int min_ready, bool drain, uint32_t* cnt) {
     const FRay f = make_fray(o, d);
@@ -1067,7 +1066,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 ref = pop();
             }
             while (leaf != kTravDone) {
-                leaf_test<Real, COUNT>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
+                leaf_test<Real, COUNT, DEFER>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
                 if (ref < 0 && ref != kTravDone) {
                     leaf = ref;
@@ -1424,7 +1423,7 @@ __device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, c
             return closest_hit_brute_nf<Real, COUNT>(S, n_prims, r, t, reinterpret_cast<float*>(stk), cnt);
         return closest_hit_brute<Real, COUNT>(S, n_prims, r, t, cnt);
     }
-    if (TRAV == TRAV_FAST) return closest_hit_fast<Real, COUNT>(S, r, t, stk, stkt, cnt);
+    if (trav_fast(TRAV)) return closest_hit_fast<Real, COUNT, TRAV == TRAV_FAST_DEFER>(S, r, t, stk, stkt, cnt);
     return closest_hit<Real, COUNT>(S, r, t, stk, cnt);
 }
 
@@ -1973,7 +1972,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     Path<EMIT> P;
     const double rtx = 1.0 / (double)tiles_x;
     // resumable fast traversal (product builds): per-lane walk state across iterations
-    constexpr bool RS = RT_RESUME && TRAV == TRAV_FAST && INSTR == 0;
+    constexpr bool RS = RT_RESUME && trav_fast(TRAV) && INSTR == 0;
     FastWalk<Real> W;
     bool walking = false;
 
@@ -2054,7 +2053,8 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 }
             }
             const bool was_walking = walking;
-            fast_walk_rounds<Real, COUNT>(S, P.o, P.d, W, walking, stk, sb.min_ready, exhausted, cnt);
+            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER>(S, P.o, P.d, W, walking, stk, sb.min_ready, exhausted,
+                                                                   cnt);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)
             if (was_walking && !walking) {
                 fast_walk_resolve<Real, COUNT>(S, P.o, P.d, W, cnt);

@@ -266,7 +266,7 @@ struct rt_camera {
         g.my_tiles = (int)mine;
         const long want = (mine + (kBlock / kWave) - 1) / (kBlock / kWave);
         g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus));  // one persistent workgroup per CU
-        const KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
+        KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
         const size_t stack = stack_lds_bytes(C.stack_depth, v.trav, C.n_prims);
         // LDS-resident scene: the BVH walk's data and the primitive records
         // (level 1), plus the material and light tables when they fit too
@@ -280,6 +280,13 @@ struct rt_camera {
             else if (v.trav == TRAV_FAST && stack + (size_t)lds_words * 16 <= lds_cap) g.lds_level = 1;
         }
         g.lds_bytes = stack + (size_t)(g.lds_level == 2 ? lds_words2 : g.lds_level == 1 ? lds_words : 0) * 16;
+        // Deferred exact sphere tests pay where the walk is VALU-bound and leaves hold
+        // several candidates: LDS-resident trees of >= 100 primitives (spheres-500
+        // +4.7 %); tiny trees have ~1 candidate per ray (rain-50 -1.3 %) and trees
+        // walked from global memory are bound by node fetches (spheres-100k -2.3 %;
+        // profiles/r02/defer/). RT_AMD_DEFER=0/1 overrides.
+        v.defer = v.trav == TRAV_FAST &&
+                  env_flag("RT_AMD_DEFER", g.lds_level >= 1 && C.n_prims >= 100);
         if (g.lds_bytes > (size_t)lds_max)
             throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile, packed ? 1 : 0};

@@ -254,18 +254,19 @@ def test_world_hit_matches_oracle(rt, oracle, gpu):
 
 
 @pytest.mark.parametrize("name", ["cornell", "spheres", "rain", "default"])
-def test_fast_traversal_equals_reference_traversal(rt, gpu, name):
-    """Larger images than the oracle can render quickly: the fast and the
-    brute-force closest hit must reproduce the reference-order traversal
-    bit-for-bit."""
+def test_fast_traversal_equals_reference_traversal(rt, gpu, name, monkeypatch):
+    """Larger images than the oracle can render quickly: the fast (with and
+    without deferred exact tests) and the brute-force closest hit must reproduce
+    the reference-order traversal bit-for-bit."""
     cfg, ro = _cfgs()[name]
     sd = rt.generate_scene_data(cfg)
     ro = {**ro, "width": 192, "samples": 16}
     outs = []
-    for trav in ["reference", "fast", "brute"]:
+    for trav, defer in [("reference", "0"), ("fast", "0"), ("brute", "0"), ("fast", "1")]:
+        monkeypatch.setenv("RT_AMD_DEFER", defer)
         cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
         outs.append((rgb, rad, st))
-    for k in (1, 2):
+    for k in (1, 2, 3):
         assert np.array_equal(outs[0][0], outs[k][0])
         assert np.array_equal(outs[0][1], outs[k][1], equal_nan=True)
         assert outs[0][2].bounces == outs[k][2].bounces
@@ -399,19 +400,21 @@ def test_tiny_scenes_every_strategy(rt, oracle, gpu, n):
         assert_stats_identical(st, orc["stats"])
 
 
-def test_large_scene_global_traversal(rt, oracle, gpu):
+def test_large_scene_global_traversal(rt, oracle, gpu, monkeypatch):
     """A scene too large for the LDS-resident copy (deeper SAH tree walked from
     global memory, chunked kernel): fast == reference traversal bit for bit,
     and hits against the oracle."""
     sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 6000, "seed": 9}})
     ro = {"width": 96, "aspect": 1, "samples": 8, "depth": 12, **NOADAPT}
     outs = []
-    for trav in ("reference", "fast"):
+    for trav, defer in (("reference", "0"), ("fast", "0"), ("fast", "1")):
+        monkeypatch.setenv("RT_AMD_DEFER", defer)
         cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
         outs.append((rgb, rad, st))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1], equal_nan=True)
-    assert outs[0][2].bounces == outs[1][2].bounces
+    for k in (1, 2):
+        assert np.array_equal(outs[0][0], outs[k][0])
+        assert np.array_equal(outs[0][1], outs[k][1], equal_nan=True)
+        assert outs[0][2].bounces == outs[k][2].bounces
     rng = np.random.default_rng(3)
     n = 4000
     o = (rng.uniform(-20, 20, (n, 3)) + np.float64([0, 2, 0])).astype(np.float32)
@@ -539,13 +542,15 @@ def _random_scene(seed):
 
 
 @pytest.mark.parametrize("seed", range(12))
-def test_random_scenes_match_oracle(rt, oracle, gpu, seed):
+def test_random_scenes_match_oracle(rt, oracle, gpu, seed, monkeypatch):
     sd = _random_scene(seed)
     ro = {"width": 32, "samples": 4, "depth": 8, **NOADAPT}
     orc = oracle.render(sd, ro)
-    for trav in ("auto", "fast", "brute", "reference"):
+    for trav, defer in (("auto", "0"), ("fast", "0"), ("fast", "1"), ("brute", "0"), ("reference", "0")):
+        monkeypatch.setenv("RT_AMD_DEFER", defer)
         cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
-        assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"random {seed} {trav} ({len(sd['objects'])} objects)")
+        assert_identical(rad, rgb, orc["radiance"], orc["rgb"],
+                         f"random {seed} {trav} defer {defer} ({len(sd['objects'])} objects)")
         assert_stats_identical(st, orc["stats"])
 
 
