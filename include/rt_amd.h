@@ -180,6 +180,14 @@ int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms);
  * sequential kernel counts as one). Passes split the per-sample record buffer. */
 int rt_camera_pass_count(rt_camera* cam, int32_t* passes);
 
+/* Path kernel of the most recent render: RT_KERNEL_NONE before any,
+ * RT_KERNEL_SEQUENTIAL (wave per 8x8 tile, adaptive sampling), RT_KERNEL_CHUNKED
+ * (lane work pool + in-order accumulate) or RT_KERNEL_POOL (stage-compacted
+ * path pools + in-order accumulate). Diagnostics and tests; no reference
+ * counterpart (the reference has one CPU loop, src/camera.ts:388-431). */
+enum { RT_KERNEL_NONE = 0, RT_KERNEL_SEQUENTIAL = 1, RT_KERNEL_CHUNKED = 2, RT_KERNEL_POOL = 3 };
+int rt_camera_last_kernel(rt_camera* cam, int32_t* kernel);
+
 /* Frees the camera's device resources (scene copy, frame and record buffers,
  * events); the next render re-creates them on the then-current device. */
 int rt_camera_release_device(rt_camera* cam);

@@ -23,12 +23,15 @@ struct LaunchGeom {
 
 // LDS budget (stack + [tnodes][prims]) up to which the scene is copied into LDS.
 constexpr int kLdsSceneMaxBytes = 152 * 1024;
+// Static LDS of the chunked / pool kernels (the phase table), beside the dynamic allocation.
+constexpr size_t kStaticLdsBytes = 512;
 
 struct KernelVariant {
     bool emit;   // emission stack (a scattering material emits)
     int count;   // 0 product, 1 work counters, 2 section timing (diagnostic)
     int trav;    // TRAV_FAST / TRAV_REFERENCE / TRAV_BRUTE (resolved, never AUTO)
     bool defer = false;  // TRAV_FAST: deferred exact sphere tests (TRAV_FAST_DEFER kernels)
+    bool pool = false;   // chunked passes run the stage-compacted pool kernel (pt_pool_kernel)
 };
 
 // sb == nullptr: the sequential-pixel kernel; else the chunked kernel over sb's pass.

@@ -6,7 +6,16 @@ namespace rt {
 
 template <bool EMIT, int INSTR, int TRAV, int LDSS>
 static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
-                      const SampleBuf* sb, hipStream_t stream) {
+                      const SampleBuf* sb, bool pool, hipStream_t stream) {
+    if (sb && pool) {  // stage-compacted pool kernel: product brute-force builds only
+        if constexpr (!EMIT && INSTR == 0 && TRAV == TRAV_BRUTE) {
+            hipLaunchKernelGGL((pt_pool_kernel<float, TRAV, LDSS>), dim3(g.grid), dim3(kBlockPool), g.lds_bytes, stream,
+                               S, reg, out, g.tiles_x, *sb);
+            return hipGetLastError();
+        } else {
+            return hipErrorInvalidValue;
+        }
+    }
     if (sb)
         hipLaunchKernelGGL((pt_chunk_kernel<float, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlockChunk), g.lds_bytes,
                            stream, S, reg, out, g.tiles_x, *sb);
@@ -18,20 +27,20 @@ static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& o
 
 template <bool EMIT, int INSTR, int TRAV>
 static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
-                     const SampleBuf* sb, hipStream_t stream) {
+                     const SampleBuf* sb, bool pool, hipStream_t stream) {
     // LDS residency levels (pt_kernel.hpp scene_prologue); never with the reference traversal
     constexpr int L1 = trav_fast(TRAV) ? 1 : 0, L2 = TRAV == TRAV_REFERENCE ? 0 : 2;
-    if (g.lds_level >= 2) return go2<EMIT, INSTR, TRAV, L2>(S, reg, out, g, sb, stream);
-    if (g.lds_level == 1) return go2<EMIT, INSTR, TRAV, L1>(S, reg, out, g, sb, stream);
-    return go2<EMIT, INSTR, TRAV, 0>(S, reg, out, g, sb, stream);
+    if (g.lds_level >= 2) return go2<EMIT, INSTR, TRAV, L2>(S, reg, out, g, sb, pool, stream);
+    if (g.lds_level == 1) return go2<EMIT, INSTR, TRAV, L1>(S, reg, out, g, sb, pool, stream);
+    return go2<EMIT, INSTR, TRAV, 0>(S, reg, out, g, sb, pool, stream);
 }
 
 template <int TRAV>
 static hipError_t go_t(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
                        const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
-    if (v.count == 2) return v.emit ? go<true, 2, TRAV>(S, reg, out, g, sb, stream) : go<false, 2, TRAV>(S, reg, out, g, sb, stream);
-    if (v.count == 1) return v.emit ? go<true, 1, TRAV>(S, reg, out, g, sb, stream) : go<false, 1, TRAV>(S, reg, out, g, sb, stream);
-    return v.emit ? go<true, 0, TRAV>(S, reg, out, g, sb, stream) : go<false, 0, TRAV>(S, reg, out, g, sb, stream);
+    if (v.count == 2) return v.emit ? go<true, 2, TRAV>(S, reg, out, g, sb, v.pool, stream) : go<false, 2, TRAV>(S, reg, out, g, sb, v.pool, stream);
+    if (v.count == 1) return v.emit ? go<true, 1, TRAV>(S, reg, out, g, sb, v.pool, stream) : go<false, 1, TRAV>(S, reg, out, g, sb, v.pool, stream);
+    return v.emit ? go<true, 0, TRAV>(S, reg, out, g, sb, v.pool, stream) : go<false, 0, TRAV>(S, reg, out, g, sb, v.pool, stream);
 }
 
 hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,

@@ -57,6 +57,7 @@ struct DevScene {
     int32_t off_tprims;                 // byte offset of tprims in the blob
     int32_t off_tsph;                   // byte offset of tsph in the blob
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
+    int32_t lds_pool_off;               // pool kernel: byte offset of the per-wave path pools (after the scene)
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
@@ -1556,6 +1557,105 @@ __device__ __forceinline__ bool path_pre(const RtCamera& C, Path<EMIT>& P, Prof&
     return term;
 }
 
+// The stages of the second half of a rayColor level (src/camera.ts:236-319),
+// shared by path_post and the stage-compacted pool kernel.
+
+// Miss: the background gradient times the throughput (camera.ts:236-244).
+template <class Real, bool EMIT, bool PROF>
+__device__ __forceinline__ V3 miss_color(const RtCamera& C, const Path<EMIT>& P, unsigned long long& st_err,
+                                         Prof& pf) {
+    if (!C.has_background) st_err |= ERR_NO_BACKGROUND;
+    const V3 ud = unit<Real>(P.d);
+    const Real a = (Real)0.5 * ((Real)ud.y + (Real)1);
+    const V3 c = mulv(add(scale<Real>(ld3(C.bg_top), (Real)1 - a), scale<Real>(ld3(C.bg_bottom), a)), P.T);
+    psec<PROF>(pf, PR_MISS);
+    return c;
+}
+
+// Hit record (sphere.ts:67-84, quad.ts:72-83, plane.ts:246-259) and the
+// material's emission and scatter (camera.ts:246-262). Returns the scatter kind;
+// `planar` = the primitive has a fixed normal (quad / plane: ONB table lookup).
+template <class Real, bool EMIT, bool COUNT, bool PROF>
+__device__ __forceinline__ int shade_hit(const DevScene& S, Path<EMIT>& P, int h, Real t, uint32_t* cnt, Prof& pf,
+                                         V3& p, V3& nrm, bool& front, bool& planar, V3& emitted, V3& att, V3& sdir) {
+    if (COUNT) cnt[CT_MATERIAL]++;
+    const RtPrim pr = S.prims[h];
+    p = ray_at<Real>(P.o, P.d, t);
+    planar = pr.type != PRIM_SPHERE;
+    if (!planar) {
+        nrm = divs<Real>(sub(p, ld3(pr.g0)), sphere_radius<Real>(pr));
+        front = dot<Real>(P.d, nrm) <= (Real)0;
+        if (!front) nrm = neg(nrm);
+    } else {
+        const V3 pn = ld3(pr.g3);
+        front = dot<Real>(P.d, pn) <= (Real)0;
+        nrm = front ? pn : neg(pn);
+    }
+    const RtMat hm = S.mats[pr.mat];
+    emitted = mulv(ld3(hm.emitted), P.T);
+    psec<PROF>(pf, PR_HITREC);
+    const int kind = scatter<Real>(S, pr.mat, P.d, nrm, front, P.rng, att, sdir);
+    psec<PROF>(pf, PR_SCATTER);
+    return kind;
+}
+
+// A diffuse (PDF) scatter: MixturePDF([CosinePDF(n), light PDFs...], [0.5,
+// 0.5/nL...]) generate + value and the throughput update (camera.ts:263-315).
+// Returns true when the path ends here (mixture value <= 0.0001: the caller's
+// sample radiance is the level's emission); else P continues from p.
+template <class Real, bool EMIT, bool COUNT, bool PROF>
+__device__ __forceinline__ bool shade_diffuse(const DevScene& S, const RtCamera& C, Path<EMIT>& P, int h, bool planar,
+                                              bool front, V3 p, V3 nrm, V3 att, uint32_t* cnt, Prof& pf) {
+    if (COUNT) cnt[CT_DIFFUSE]++;
+    Onb b;
+    if (planar && h < S.n_onb) {
+        const RtOnb& ob = S.onbs[(h * 2 + (sizeof(Real) == 4 ? 1 : 0)) * 2 + (front ? 0 : 1)];
+        b.u = ld3(ob.u);
+        b.v = ld3(ob.v);
+        b.w = ld3(ob.w);
+    } else {
+        b = make_onb<Real>(nrm);
+    }
+    const Real total = (Real)S.mix_total;
+    const Real lw = (Real)S.light_w;
+    const Real rnd = uniform<Real>(P.rng) * total;
+    Real partial = (Real)0.5;
+    V3 gdir;
+    if (rnd < partial || C.n_lights == 0) {
+        const Real r1 = uniform<Real>(P.rng);
+        const Real r2 = uniform<Real>(P.rng);
+        const Real phi = (Real)2 * K<Real>::PI * r1;
+        const Real sr2 = m_sqrt(r2);
+        Real sn, cs;
+        m_sincos(phi, sn, cs);
+        gdir = onb_local<Real>(b, mk<Real>(cs * sr2, sn * sr2, m_sqrt((Real)1 - r2)));
+    } else {
+        int pick = C.n_lights - 1;
+        for (int l = 0; l < C.n_lights; ++l) {
+            partial += lw;
+            if (rnd < partial) { pick = l; break; }
+        }
+        gdir = light_generate<Real>(S, S.lights[pick], p, P.rng);  // pick: per lane
+    }
+    psec<PROF>(pf, PR_SAMPLE);
+    const Real cv = cosine_value<Real>(b, gdir);
+    Real sum = (Real)0.5 * cv;
+    for (int l = 0; l < C.n_lights; ++l)
+        sum += lw * light_pdf_value<Real, COUNT, true>(S, ld_uniform(S.glights, l), p, gdir, cnt);
+    const Real pv = sum / total;
+    bool term = false;
+    if (pv <= (Real)0.0001) {
+        term = true;
+    } else {
+        const V3 brdf = scale<Real>(att, cv);
+        P.T = divs<Real>(mulv(P.T, brdf), pv);
+        P.o = p;
+        P.d = gdir;
+    }
+    psec<PROF>(pf, PR_PDF);
+    return term;
+}
+
 // Second half: given the closest hit (h, t) of the path's ray, the miss /
 // emission / scatter / light sampling of the same level (src/camera.ts:236-319).
 // Returns true when the path ends (`c` = the sample's radiance).
@@ -1564,102 +1664,31 @@ __device__ __forceinline__ bool path_post(const DevScene& S, const RtCamera& C, 
                                           uint32_t* cnt, unsigned long long& st_err, Prof& pf, V3& c) {
     bool term = false;
     c = v3(0, 0, 0);
-    {
-        {
-            if (h < 0) {
+    if (h < 0) {
+        term = true;
+        c = miss_color<Real, EMIT, PROF>(C, P, st_err, pf);
+    } else {
+        V3 p, nrm, emitted, att, sdir;
+        bool front, planar;
+        const int kind = shade_hit<Real, EMIT, COUNT, PROF>(S, P, h, t, cnt, pf, p, nrm, front, planar, emitted, att,
+                                                            sdir);
+        if (kind == SC_NONE) {
+            term = true;
+            c = emitted;
+        } else {
+            ++P.bounces;
+            if (kind == SC_SPEC) {
+                P.T = mulv(P.T, att);
+                P.o = p;
+                P.d = sdir;
+            } else if (shade_diffuse<Real, EMIT, COUNT, PROF>(S, C, P, h, planar, front, p, nrm, att, cnt, pf)) {
                 term = true;
-                if (!C.has_background) st_err |= ERR_NO_BACKGROUND;
-                const V3 ud = unit<Real>(P.d);
-                const Real a = (Real)0.5 * ((Real)ud.y + (Real)1);
-                c = mulv(add(scale<Real>(ld3(C.bg_top), (Real)1 - a), scale<Real>(ld3(C.bg_bottom), a)), P.T);
-                psec<PROF>(pf, PR_MISS);
-            } else {
-                if (COUNT) cnt[CT_MATERIAL]++;
-                // hit record (sphere.ts:67-84, quad.ts:72-83, plane.ts:246-259)
-                const RtPrim pr = S.prims[h];
-                const V3 p = ray_at<Real>(P.o, P.d, t);
-                V3 nrm;
-                bool front;
-                if (pr.type == PRIM_SPHERE) {
-                    nrm = divs<Real>(sub(p, ld3(pr.g0)), sphere_radius<Real>(pr));
-                    front = dot<Real>(P.d, nrm) <= (Real)0;
-                    if (!front) nrm = neg(nrm);
-                } else {
-                    const V3 pn = ld3(pr.g3);
-                    front = dot<Real>(P.d, pn) <= (Real)0;
-                    nrm = front ? pn : neg(pn);
-                }
-                const RtMat hm = S.mats[pr.mat];
-                const V3 emitted = mulv(ld3(hm.emitted), P.T);
-                V3 att, sdir;
-                psec<PROF>(pf, PR_HITREC);
-                const int kind = scatter<Real>(S, pr.mat, P.d, nrm, front, P.rng, att, sdir);
-                psec<PROF>(pf, PR_SCATTER);
-                if (kind == SC_NONE) {
-                    term = true;
-                    c = emitted;
-                } else {
-                    ++P.bounces;
-                    if (kind == SC_SPEC) {
-                        P.T = mulv(P.T, att);
-                        P.o = p;
-                        P.d = sdir;
-                    } else {
-                        if (COUNT) cnt[CT_DIFFUSE]++;
-                        // MixturePDF([CosinePDF(n), light pdfs...], [0.5, 0.5/nL...])
-                        Onb b;
-                        if (pr.type != PRIM_SPHERE && h < S.n_onb) {
-                            const RtOnb& ob = S.onbs[(h * 2 + (sizeof(Real) == 4 ? 1 : 0)) * 2 + (front ? 0 : 1)];
-                            b.u = ld3(ob.u);
-                            b.v = ld3(ob.v);
-                            b.w = ld3(ob.w);
-                        } else {
-                            b = make_onb<Real>(nrm);
-                        }
-                        const Real total = (Real)S.mix_total;
-                        const Real lw = (Real)S.light_w;
-                        const Real rnd = uniform<Real>(P.rng) * total;
-                        Real partial = (Real)0.5;
-                        V3 gdir;
-                        if (rnd < partial || C.n_lights == 0) {
-                            const Real r1 = uniform<Real>(P.rng);
-                            const Real r2 = uniform<Real>(P.rng);
-                            const Real phi = (Real)2 * K<Real>::PI * r1;
-                            const Real sr2 = m_sqrt(r2);
-                            Real sn, cs;
-                            m_sincos(phi, sn, cs);
-                            gdir = onb_local<Real>(b, mk<Real>(cs * sr2, sn * sr2, m_sqrt((Real)1 - r2)));
-                        } else {
-                            int pick = C.n_lights - 1;
-                            for (int l = 0; l < C.n_lights; ++l) {
-                                partial += lw;
-                                if (rnd < partial) { pick = l; break; }
-                            }
-                            gdir = light_generate<Real>(S, S.lights[pick], p, P.rng);  // pick: per lane
-                        }
-                        psec<PROF>(pf, PR_SAMPLE);
-                        const Real cv = cosine_value<Real>(b, gdir);
-                        Real sum = (Real)0.5 * cv;
-                        for (int l = 0; l < C.n_lights; ++l)
-                            sum += lw * light_pdf_value<Real, COUNT, true>(S, ld_uniform(S.glights, l), p, gdir, cnt);
-                        const Real pv = sum / total;
-                        if (pv <= (Real)0.0001) {
-                            term = true;
-                            c = emitted;
-                        } else {
-                            const V3 brdf = scale<Real>(att, cv);
-                            P.T = divs<Real>(mulv(P.T, brdf), pv);
-                            P.o = p;
-                            P.d = gdir;
-                        }
-                        psec<PROF>(pf, PR_PDF);
-                    }
-                    if (EMIT && !term) {
-                        if (P.em_n < kEmitStack) P.em[P.em_n] = emitted;
-                        else st_err |= ERR_EMIT_STACK;
-                        ++P.em_n;
-                    }
-                }
+                c = emitted;
+            }
+            if (EMIT && !term) {
+                if (P.em_n < kEmitStack) P.em[P.em_n] = emitted;
+                else st_err |= ERR_EMIT_STACK;
+                ++P.em_n;
             }
         }
     }
@@ -1937,6 +1966,43 @@ __device__ __forceinline__ void item_pixel(const RtRegion& reg, int tiles_x, dou
     j = reg.y + ty * kTile + (l / kTile);
 }
 
+// The guided schedule's phase rows, copied to LDS at kernel start: an item's
+// phase is per lane, and indexing the kernel-argument arrays by it costs a
+// select chain per field (and SGPRs the path code then spills).
+struct PhaseRow {
+    int32_t s0, chunk, nch, base;
+    double rnch;
+    int32_t pad[2];
+};
+__device__ __forceinline__ void phase_table_init(const SampleBuf& sb, PhaseRow* tab) {
+    const int t = threadIdx.x;
+    if (t < kMaxPhases) {
+        PhaseRow r;
+        r.s0 = sb.s0[t];
+        r.chunk = sb.chunk[t];
+        r.nch = sb.nch[t];
+        r.base = t < sb.n_phases ? sb.item_base[t] : 0x7fffffff;
+        r.rnch = sb.rnch[t];
+        r.pad[0] = r.pad[1] = 0;
+        tab[t] = r;
+    }
+    __syncthreads();
+}
+// Item u of the launch -> (tile among this pass's tiles, lane-pixel l, sample range [s, s_end)).
+__device__ __forceinline__ void item_decode(const SampleBuf& sb, const PhaseRow* tab, int u, int& tl, int& l, int& s,
+                                            int& s_end) {
+    int ph = 0;
+    for (int q = 1; q < sb.n_phases; ++q) ph += u >= tab[q].base ? 1 : 0;
+    const PhaseRow r = tab[ph];
+    const int v = u - r.base;  // item within the phase: (tile, chunk) groups of 64
+    const int q = v >> 6;
+    l = v & 63;
+    tl = udiv(q, r.nch, r.rnch);
+    const int ch = q - tl * r.nch;
+    s = r.s0 + ch * r.chunk;
+    s_end = s + r.chunk;
+}
+
 template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
 __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRegion reg, RenderOut out,
                                                                         int tiles_x, SampleBuf sb) {
@@ -1944,6 +2010,8 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     constexpr bool PROF = INSTR == 2;
     extern __shared__ int lds_stack[];
     const RtCamera& C0 = S0.cam;
+    __shared__ PhaseRow ptab[kMaxPhases];
+    phase_table_init(sb, ptab);
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
     int* stk = lds_stack + threadIdx.x;
@@ -1998,18 +2066,13 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 if (slot < 0 && rank < take) {
-                    const int u = pool_next + rank;
-                    int ph = 0;
-                    for (int k = 1; k < sb.n_phases; ++k)
-                        if (u >= sb.item_base[k]) ph = k;
-                    const int v = u - sb.item_base[ph];  // item within the phase: (tile, chunk) groups of 64
-                    const int q = v >> 6, l = v & 63;
-                    const int tl = udiv(q, sb.nch[ph], sb.rnch[ph]), ch = q - tl * sb.nch[ph];
+                    int tl, l, s1, e1;
+                    item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
                     item_pixel(reg, tiles_x, rtx, sb.tile0 + tl, l, i, j);
                     if (i < endX && j < endY) {
                         slot = tl * 64 + l;
-                        s = sb.s0[ph] + ch * sb.chunk[ph];
-                        s_end = s + sb.chunk[ph];
+                        s = s1;
+                        s_end = e1;
                         pix = (uint32_t)j * (uint32_t)C0.width + (uint32_t)i;
                         pc = pixel_center<Real>(cam_opaque(), i, j);
                         new_path = true;
@@ -2093,6 +2156,254 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     PixStats st;
     publish_stats(out, st, st_err, lane);
     publish_counters<COUNT, PROF>(out, cnt, pf, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Stage-compacted pool kernel (fixed spp, no emission stack): the chunked
+// kernel's work items and per-sample records, but lanes are not tied to paths.
+// Each wave keeps kPoolK path slots in LDS and two queues of slot indices:
+//   A (trace): start the sample's path (getRay) or continue it, depth cut-off /
+//     roulette, closest hit, miss or hit record + material scatter;
+//   D (diffuse): the mixture-PDF light sampling, its value and the throughput
+//     update (src/camera.ts:263-315), which about half of the hits need.
+// Every trip runs ONE stage on up to 64 queued paths (ballot/mbcnt queue
+// appends): D once 64 paths wait (or when it is the longer queue), A
+// otherwise. So the diffuse shading runs on full waves rather than on the
+// lanes whose path happens to need it in a given trip (the north star's
+// persistent-wavefront work queues). Each path's arithmetic and draw order are
+// path_trip's, so every sample record - and the image - is bit-identical.
+// ---------------------------------------------------------------------------
+#ifndef RT_POOL_K
+#define RT_POOL_K 96
+#endif
+#ifndef RT_POOL_BLOCK
+#define RT_POOL_BLOCK 1024
+#endif
+constexpr int kPoolK = RT_POOL_K;          // path slots per wave
+constexpr int kBlockPool = RT_POOL_BLOCK;  // persistent workgroup size
+constexpr int kPoolGroups = 5;             // 16-byte groups per slot (below)
+static_assert(kPoolK >= kWave && kPoolK <= 256, "pool slots: one full wave, u8 queue entries");
+// Per wave: slot state as [group][slot] float4, then the A and D queues (u8 slot indices).
+//   g0 {rng lo, rng hi, phase, s_end}  phase: bounces so far (>= 0), PH_NEW or PH_ITEM
+//   g1 {o (hit point p when queued for D), slot}
+//   g2 {d (the face normal when queued for D), s}
+//   g3 {T, i | j << 16}
+//   g4 {attenuation, h | planar << 30 | front << 31}   (D only)
+constexpr size_t kPoolWaveBytes = ((size_t)kPoolK * kPoolGroups * 16 + 2 * kPoolK + 15) / 16 * 16;
+constexpr size_t pool_lds_bytes() { return (size_t)(kBlockPool / kWave) * kPoolWaveBytes; }
+enum : int { PH_NEW = -1, PH_ITEM = -2 };  // next sample's path to start / no work item
+
+__device__ __forceinline__ int pool_ring(int x) { return x >= kPoolK ? x - kPoolK : x; }
+
+// Appends slot k of every lane with `want` to a queue (head, cnt wave-uniform).
+__device__ __forceinline__ void queue_push(uint8_t* q, int head, int& cnt, bool want, int k) {
+    const unsigned long long m = __ballot(want);
+    if (want) {
+        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        q[pool_ring(pool_ring(head + cnt) + r)] = (uint8_t)k;
+    }
+    cnt += __popcll(m);
+}
+
+template <class Real, int TRAV, int LDSS>
+__global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
+                                                               SampleBuf sb) {
+    extern __shared__ int lds_stack[];
+    const RtCamera& C0 = S0.cam;
+    __shared__ PhaseRow ptab[kMaxPhases];
+    phase_table_init(sb, ptab);
+    const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
+    const int lane = threadIdx.x & (kWave - 1);
+    int* stk = lds_stack + threadIdx.x;
+    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kStackStride + threadIdx.x;
+    char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * kPoolWaveBytes;
+    float4* G = reinterpret_cast<float4*>(wpool);  // group q of slot k: G[q * kPoolK + k]
+    uint8_t* qa = reinterpret_cast<uint8_t*>(wpool + (size_t)kPoolK * kPoolGroups * 16);
+    uint8_t* qd = qa + kPoolK;
+    const int endX = min(reg.x + reg.width, C0.width);
+    const int endY = min(reg.y + reg.height, C0.height);
+    const int n_items = sb.n_items;
+    const double rtx = 1.0 / (double)tiles_x;
+    uint32_t* cnt = nullptr;  // product build: no work counters
+    unsigned long long st_err = 0;
+    Prof pf;
+
+    for (int k = lane; k < kPoolK; k += kWave) {
+        qa[k] = (uint8_t)k;
+        G[k] = make_float4(0.f, 0.f, __int_as_float(PH_ITEM), 0.f);
+    }
+    int a_head = 0, a_cnt = kPoolK, d_head = 0, d_cnt = 0;  // wave-uniform queue state
+    int pool_next = 0, pool_end = 0;                       // wave-uniform item hand-out
+    bool exhausted = false;
+
+    // the sample's radiance and bounce count to its record; the slot's next phase
+    auto record = [&](V3 c, int bounces, int slot, int& s, int s_end) -> int {
+        float4 r;
+        r.x = c.x;
+        r.y = c.y;
+        r.z = c.z;
+        r.w = __int_as_float(bounces);
+        sb.rec[(size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot] = r;
+        ++s;
+        return s < s_end ? PH_NEW : PH_ITEM;
+    };
+
+    while (a_cnt + d_cnt > 0) {
+        // other lanes' slot and queue writes of the previous trip (one wave: LDS is in order)
+        __asm__ volatile("" ::: "memory");
+        if (d_cnt >= kWave || d_cnt > a_cnt) {
+            // ---- D: diffuse shading of up to 64 queued paths ----
+            const int n = min(kWave, d_cnt);
+            const int k = lane < n ? (int)qd[pool_ring(d_head + lane)] : -1;
+            d_head = pool_ring(d_head + n);
+            d_cnt -= n;
+            if (k >= 0) {
+                const float4 g0 = G[k], g1 = G[kPoolK + k], g2 = G[2 * kPoolK + k], g3 = G[3 * kPoolK + k],
+                             g4 = G[4 * kPoolK + k];
+                Path<false> P;
+                P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
+                P.bounces = __float_as_int(g0.z);
+                P.em_n = 0;
+                P.o = V3{g1.x, g1.y, g1.z};
+                P.d = V3{g2.x, g2.y, g2.z};
+                P.T = V3{g3.x, g3.y, g3.z};
+                const int hf = __float_as_int(g4.w);
+                const int h = hf & 0x3fffffff;
+                const int s_end = __float_as_int(g0.w), slot = __float_as_int(g1.w);
+                int s = __float_as_int(g2.w);
+                int phase = P.bounces;
+                const RtCamera& C = cam_opaque();
+                if (shade_diffuse<Real, false, false, false>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
+                                                             V3{g4.x, g4.y, g4.z}, cnt, pf)) {
+                    // mixture value cut-off: the level's emission (as computed at the hit: T is unchanged)
+                    const V3 c = mulv(ld3(S.mats[S.prims[h].mat].emitted), P.T);
+                    phase = record(c, P.bounces, slot, s, s_end);
+                }
+                G[k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
+                                   __int_as_float(phase), g0.w);
+                G[kPoolK + k] = make_float4(P.o.x, P.o.y, P.o.z, g1.w);
+                G[2 * kPoolK + k] = make_float4(P.d.x, P.d.y, P.d.z, __int_as_float(s));
+                G[3 * kPoolK + k] = make_float4(P.T.x, P.T.y, P.T.z, g3.w);
+            }
+            queue_push(qa, a_head, a_cnt, k >= 0, k);
+        } else {
+            // ---- A: trace up to 64 queued paths ----
+            const int n = min(kWave, a_cnt);
+            const int k = lane < n ? (int)qa[pool_ring(a_head + lane)] : -1;
+            a_head = pool_ring(a_head + n);
+            a_cnt -= n;
+            float4 g0 = make_float4(0.f, 0.f, __int_as_float(PH_ITEM), 0.f), g1 = g0, g2 = g0, g3 = g0;
+            if (k >= 0) {
+                g0 = G[k];
+                g1 = G[kPoolK + k];
+                g2 = G[2 * kPoolK + k];
+                g3 = G[3 * kPoolK + k];
+            }
+            int phase = __float_as_int(g0.z), s_end = __float_as_int(g0.w), slot = __float_as_int(g1.w);
+            int s = __float_as_int(g2.w), ij = __float_as_int(g3.w);
+            // work items for slots without one (the chunked kernel's guided hand-out)
+            const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
+            if (need != 0ull && !exhausted) {
+                if (pool_next >= pool_end) {
+                    int base = 0;
+                    if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
+                    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+                    if (base >= n_items) {
+                        exhausted = true;
+                    } else {
+                        pool_next = base;
+                        pool_end = min(base + sb.pool, n_items);
+                    }
+                }
+                if (!exhausted) {
+                    const int take = min(__popcll(need), pool_end - pool_next);
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                    if (k >= 0 && phase == PH_ITEM && rank < take) {
+                        int tl, l, s1, e1, i, j;
+                        item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
+                        item_pixel(reg, tiles_x, rtx, sb.tile0 + tl, l, i, j);
+                        if (i < endX && j < endY) {
+                            slot = tl * 64 + l;
+                            s = s1;
+                            s_end = e1;
+                            ij = i | (j << 16);
+                            phase = PH_NEW;
+                        }
+                    }
+                    pool_next += take;
+                }
+            }
+            const bool keep = k >= 0 && (phase != PH_ITEM || !exhausted);  // drained slots leave the pool
+            bool to_d = false;
+            if (k >= 0 && phase != PH_ITEM) {
+                const RtCamera& C = cam_opaque();
+                Path<false> P;
+                if (phase == PH_NEW) {
+                    const int i = ij & 0xffff, j = ij >> 16;
+                    path_begin<Real, false>(C, P, pixel_center<Real>(C, i, j),
+                                            (uint32_t)j * (uint32_t)C.width + (uint32_t)i, (uint32_t)s);
+                } else {
+                    P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
+                    P.o = V3{g1.x, g1.y, g1.z};
+                    P.d = V3{g2.x, g2.y, g2.z};
+                    P.T = V3{g3.x, g3.y, g3.z};
+                    P.bounces = phase;
+                    P.em_n = 0;
+                }
+                V3 c;
+                bool term = path_pre<Real, false, false>(C, P, pf, c);
+                V3 att;
+                int hf = 0;
+                if (!term) {
+                    const RayK<Real> ray = make_ray<Real>(P.o, P.d);
+                    Real t;
+                    const int h = closest_hit_any<Real, false, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
+                    if (h < 0) {
+                        term = true;
+                        c = miss_color<Real, false, false>(C, P, st_err, pf);
+                    } else {
+                        V3 p, nrm, emitted, sdir;
+                        bool front, planar;
+                        const int kind = shade_hit<Real, false, false, false>(S, P, h, t, cnt, pf, p, nrm, front,
+                                                                              planar, emitted, att, sdir);
+                        if (kind == SC_NONE) {
+                            term = true;
+                            c = emitted;
+                        } else {
+                            ++P.bounces;
+                            P.o = p;
+                            if (kind == SC_SPEC) {
+                                P.T = mulv(P.T, att);
+                                P.d = sdir;
+                            } else {
+                                to_d = true;
+                                P.d = nrm;  // queued for D: g2 carries the face normal
+                                hf = h | (planar ? (1 << 30) : 0) | (front ? (int)0x80000000 : 0);
+                            }
+                        }
+                    }
+                }
+                phase = term ? record(c, P.bounces, slot, s, s_end) : P.bounces;
+                g0 = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
+                                 __int_as_float(phase), __int_as_float(s_end));
+                g1 = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
+                g2 = make_float4(P.d.x, P.d.y, P.d.z, __int_as_float(s));
+                g3 = make_float4(P.T.x, P.T.y, P.T.z, __int_as_float(ij));
+                if (to_d) G[4 * kPoolK + k] = make_float4(att.x, att.y, att.z, __int_as_float(hf));
+            }
+            if (keep) {
+                G[k] = g0;
+                G[kPoolK + k] = g1;
+                G[2 * kPoolK + k] = g2;
+                G[3 * kPoolK + k] = g3;
+            }
+            queue_push(qa, a_head, a_cnt, keep && !to_d, k);
+            queue_push(qd, d_head, d_cnt, to_d, k);
+        }
+    }
+    PixStats st;
+    publish_stats(out, st, st_err, lane);
 }
 
 }  // namespace rt

@@ -118,6 +118,7 @@ struct rt_camera {
     std::vector<hipEvent_t> ev;
     int n_passes = 0;
     bool ev_accum = false;
+    int last_kernel = RT_KERNEL_NONE;
     unsigned long long* d_stats = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned int* d_tile = nullptr;
@@ -287,11 +288,12 @@ struct rt_camera {
         // profiles/r02/defer/). RT_AMD_DEFER=0/1 overrides.
         v.defer = v.trav == TRAV_FAST &&
                   env_flag("RT_AMD_DEFER", g.lds_level >= 1 && C.n_prims >= 100);
-        if (g.lds_bytes > (size_t)lds_max)
+        if (g.lds_bytes + kStaticLdsBytes > (size_t)lds_max)
             throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile, packed ? 1 : 0};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
         n_passes = 0;
+        last_kernel = RT_KERNEL_NONE;
         if (mine == 0) return;
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
@@ -313,6 +315,7 @@ struct rt_camera {
             hip_check(hipEventRecord(pass_event(0, 1), stream), "hipEventRecord");
             n_passes = 1;
             ev_accum = false;
+            last_kernel = RT_KERNEL_SEQUENTIAL;
             return;
         }
         // chunked kernel: passes over at most sbuf_budget bytes of per-sample records
@@ -372,6 +375,15 @@ struct rt_camera {
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
         }
+        // Stage-compacted pool kernel (pt_pool_kernel): possible for product brute-force
+        // launches without an emission stack whose per-wave path pools fit in LDS beside
+        // the scene; the default in ref precision, where the diffuse stage it compacts is
+        // heaviest (Cornell 800^2 spp256: 19.15 vs 19.23 ms; fp32 15.48 vs 14.70 ms,
+        // profiles/r02/pool/). RT_AMD_POOL_KERNEL=0/1 overrides.
+        S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
+        v.pool = !v.emit && count == 0 && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
+                 (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
+                 env_flag("RT_AMD_POOL_KERNEL", prec == PREC_REF);
         int pass = 0;
         for (long t0 = 0; t0 < mine; t0 += pass_tiles, ++pass) {
             const long nt = std::min(pass_tiles, mine - t0);
@@ -394,7 +406,8 @@ struct rt_camera {
             sb.n_items = (int32_t)items;
             if (t0 > 0) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = g;
-            gp.grid = (int)std::max<long>(1, std::min<long>(items / kBlockChunk + 1, (long)cus));
+            gp.grid = (int)std::max<long>(1, std::min<long>(items / (v.pool ? kBlockPool : kBlockChunk) + 1, (long)cus));
+            if (v.pool) gp.lds_bytes = (size_t)S.lds_pool_off + pool_lds_bytes();
             // per-pass events: path kernel [0, 1), accumulate [1, 2)
             hip_check(hipEventRecord(pass_event(pass, 0), stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, gp, &sb, stream)
@@ -406,6 +419,7 @@ struct rt_camera {
         }
         n_passes = pass;
         ev_accum = true;
+        last_kernel = v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
     }
 
     // Per-sample record buffer of the chunked kernel (grown on demand, kept).
@@ -742,6 +756,13 @@ int rt_camera_pass_count(rt_camera* cam, int32_t* passes) {
     if (!cam || !passes) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
     *passes = cam->n_passes;
+    return RT_OK;
+}
+
+int rt_camera_last_kernel(rt_camera* cam, int32_t* kernel) {
+    if (!cam || !kernel) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    *kernel = cam->last_kernel;
     return RT_OK;
 }
 

@@ -87,6 +87,7 @@ _SIGS = {
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "rt_camera_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "rt_camera_pass_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    "rt_camera_last_kernel": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rt_camera_release_device": (C.c_int, [C.c_void_p]),
     "rt_build_id": (C.c_char_p, []),
     "rt_tiles_unpack": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(RtRegion), C.c_int32, C.c_int32,

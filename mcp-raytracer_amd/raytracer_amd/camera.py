@@ -197,6 +197,15 @@ class Camera:
         _lib.check(self._lib.rt_camera_pass_count(self._h, C.byref(n)))
         return int(n.value)
 
+    KERNELS = ("none", "sequential", "chunked", "pool")
+
+    def last_kernel(self) -> str:
+        """Path kernel of the last render (rt_camera_last_kernel): 'sequential',
+        'chunked' or 'pool' ('none' before any)."""
+        n = C.c_int32()
+        _lib.check(self._lib.rt_camera_last_kernel(self._h, C.byref(n)))
+        return self.KERNELS[int(n.value)]
+
     def release_device(self) -> None:
         """Free the device copies; the next render re-creates them (rt_camera_release_device)."""
         _lib.check(self._lib.rt_camera_release_device(self._h))

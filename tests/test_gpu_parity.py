@@ -372,6 +372,42 @@ def test_chunked_kernel_equals_sequential(rt, gpu, name, monkeypatch):
     assert outs[0][2].samples == outs[1][2].samples and outs[0][2].bounces == outs[1][2].bounces
 
 
+def _pool_cases():
+    sd_c = {"type": "cornell"}
+    return [
+        ("cornell ref", sd_c, {"width": 164, "samples": 37, "depth": 16}, "ref"),  # partial tiles, every phase
+        ("cornell fp32", sd_c, {"width": 96, "samples": 64, "depth": 16}, "fp32"),
+        ("cornell d100 spp1", sd_c, {"width": 72, "samples": 1, "depth": 100}, "ref"),
+        ("tiny1", 1, {"width": 40, "samples": 9, "depth": 6}, "ref"),
+        ("tiny5", 5, {"width": 56, "samples": 9, "depth": 6}, "ref"),
+    ]
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_pool_kernel_equals_chunked_kernel(rt, gpu, case, monkeypatch):
+    """The stage-compacted pool kernel (per-wave path pools, A/D queues) writes
+    the chunked kernel's per-sample records, so images and stats are identical;
+    also a region render and a tile-group share."""
+    what, cfg, ro, prec = _pool_cases()[case]
+    sd = _tiny_scene(cfg) if isinstance(cfg, int) else rt.generate_scene_data(cfg)
+    ro = {**ro, **NOADAPT, "traversal": "brute"}
+    monkeypatch.setenv("RT_AMD_CHUNKED", "1")
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RT_AMD_POOL_KERNEL", flag)
+        cam, rgb, rad, st = _render_gpu(rt, sd, ro, precision=prec)
+        assert cam.last_kernel() == ("pool" if flag == "1" else "chunked"), what
+        W, H = cam.image_width, cam.image_height
+        reg = (5, 3, W - 9, H - 6)
+        _, rgb_r, rad_r, st_r = _render_gpu(rt, sd, ro, precision=prec, region=reg)
+        outs.append((rgb, rad, st, rgb_r, rad_r, st_r))
+    a, b = outs
+    assert_identical(a[1], a[0], b[1], b[0], f"pool vs chunked: {what}")
+    assert_identical(a[4], a[3], b[4], b[3], f"pool vs chunked region: {what}")
+    for sa, sb in ((a[2], b[2]), (a[5], b[5])):
+        assert sa.pixels == sb.pixels and sa.samples == sb.samples and sa.bounces == sb.bounces
+
+
 def _tiny_scene(n):
     objs = [{"type": "sphere", "pos": [0.9 * k - 0.9, 0.3 * (k % 2), -0.2 * k], "r": 0.45, "material": "m"}
             for k in range(n)]

@@ -18,18 +18,23 @@ import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
 from pathlib import Path
 
 root = Path(sys.argv[1])
 cfgs = sys.argv[2:]
-out_path = Path(sys.argv[0]).resolve().parents[1] / "profiles" / "pmc_valu.json"
+# PMC_VALU_OUT: another output file (A/B runs); PMC_TAG: suffix of the configuration key
+out_path = Path(os.environ.get("PMC_VALU_OUT") or Path(sys.argv[0]).resolve().parents[1] / "profiles" / "pmc_valu.json")
+TAG = os.environ.get("PMC_TAG", "")
 data = json.loads(out_path.read_text()) if out_path.exists() else {}
 F64_PEAK, F32_PEAK, SIMDS = 78.6, 157.3, 1024
 
 
 def dominant(name):
+    if re.search(r"pt_pool_kernel<", name):
+        return "pt_pool_kernel"  # product-only kernel
     m = re.search(r"(pt_chunk_kernel|pt_render_kernel)<([^>(]*)>", name)
     if not m or [a.strip() for a in m.group(2).split(",")][2] != "0":
         return None  # other kernels / instrumented builds (template args: Real, EMIT, INSTR, TRAV, LDSS)
@@ -66,7 +71,7 @@ for n, args in enumerate(cfgs, 1):
         if not pd.is_dir():
             continue
         for (k, _), cs in pass_counters(pd).items():
-            kern = k if kern is None or k == "pt_chunk_kernel" else kern
+            kern = k if kern is None or k in ("pt_chunk_kernel", "pt_pool_kernel") else kern
             for c, v in cs.items():
                 acc[(k, c)].append(v)
         for k, v in pass_durations(pd).items():
@@ -90,7 +95,7 @@ for n, args in enumerate(cfgs, 1):
     f64_flops = (c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + 2 * c["SQ_INSTS_VALU_FMA_F64"]) * 64 * lane
     f32_flops = (c["SQ_INSTS_VALU_ADD_F32"] + c["SQ_INSTS_VALU_MUL_F32"] + 2 * c["SQ_INSTS_VALU_FMA_F32"]) * 64 * lane
     cfg = line["config"]
-    key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_spp{cfg['spp']}_d{cfg['depth']}_{cfg['precision']}_n{line['n_gpus']}"
+    key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_spp{cfg['spp']}_d{cfg['depth']}_{cfg['precision']}_n{line['n_gpus']}{TAG}"
     samples = cfg["width"] * cfg["height"] * cfg["spp"]
     entry = {
         "kernel": kern, "duration_ms": round(dur * 1e3, 4), "clock_ghz": round(clock / 1e9, 3),
