@@ -68,6 +68,9 @@ struct DevScene {
 // Stats words (u64): pixels, samples total, samples min, samples max,
 // bounces total, bounces min, bounces max, error flags.
 enum { ST_PIXELS = 0, ST_SAMPLES, ST_SMIN, ST_SMAX, ST_BOUNCES, ST_BMIN, ST_BMAX, ST_ERROR, ST_WORDS };
+// Each stats word on a 128-byte line of its own (stats[k * kStatStride]): the atomics of
+// thousands of waves on one line serialise (~90 per us per line).
+constexpr int kStatStride = 16;
 // Instrumentation words (u64): the algorithmic-work counts of SURVEY.md §8d.
 enum {
     CT_NODE = 0, CT_SPHERE, CT_QUAD, CT_PLANE, CT_MATERIAL, CT_LIGHT_QUAD, CT_LIGHT_SPHERE,
@@ -94,7 +97,7 @@ struct RenderOut {
     float* radiance;     // W*H*3, may be null
     int32_t* px_samples; // W*H, may be null
     int32_t* px_bounces; // W*H, may be null
-    unsigned long long* stats;     // ST_WORDS
+    unsigned long long* stats;     // ST_WORDS words, kStatStride apart
     unsigned long long* counters;  // kCounterWords (instrumented builds only)
     unsigned int* tile_counter;
     // 0: outputs in full-frame layout (index j*W + i); 1: tile-packed slab, the
@@ -1751,25 +1754,34 @@ __device__ __forceinline__ void finish_pixel(const RtCamera& C, const RenderOut&
     st.bmax = max(st.bmax, (unsigned long long)bmax);
 }
 
-// RenderStats.merge (renderStats.ts:42-64): one atomic per wave.
+// RenderStats.merge (renderStats.ts:42-64): one atomic per word per wave.
+__device__ __forceinline__ void stats_atomics(const RenderOut& out, unsigned long long sp, unsigned long long ss,
+                                              unsigned long long smn, unsigned long long smx, unsigned long long sb,
+                                              unsigned long long bmn, unsigned long long bmx, unsigned long long err) {
+    unsigned long long* w = out.stats;
+    if (sp > 0) {
+        atomicAdd(&w[ST_PIXELS * kStatStride], sp);
+        atomicAdd(&w[ST_SAMPLES * kStatStride], ss);
+        atomicMin(&w[ST_SMIN * kStatStride], smn);
+        atomicMax(&w[ST_SMAX * kStatStride], smx);
+        atomicAdd(&w[ST_BOUNCES * kStatStride], sb);
+        atomicMin(&w[ST_BMIN * kStatStride], bmn);
+        atomicMax(&w[ST_BMAX * kStatStride], bmx);
+    }
+    if (err) atomicOr(&w[ST_ERROR * kStatStride], err);
+}
+__device__ __forceinline__ unsigned long long wave_or(unsigned long long v) {
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) v |= __shfl_xor(v, k, 64);
+    return v;
+}
 __device__ __forceinline__ void publish_stats(const RenderOut& out, const PixStats& st, unsigned long long st_err,
                                               int lane) {
     const unsigned long long sp = wave_sum(st.pixels), ss = wave_sum(st.samples), sb = wave_sum(st.b);
     const unsigned long long smn = wave_min(st.smin), smx = wave_max(st.smax);
     const unsigned long long bmn = wave_min(st.bmin), bmx = wave_max(st.bmax);
-    unsigned long long err = st_err;
-#pragma unroll
-    for (int k = 32; k > 0; k >>= 1) err |= __shfl_xor(err, k, 64);
-    if (lane == 0 && sp > 0) {
-        atomicAdd(&out.stats[ST_PIXELS], sp);
-        atomicAdd(&out.stats[ST_SAMPLES], ss);
-        atomicMin(&out.stats[ST_SMIN], smn);
-        atomicMax(&out.stats[ST_SMAX], smx);
-        atomicAdd(&out.stats[ST_BOUNCES], sb);
-        atomicMin(&out.stats[ST_BMIN], bmn);
-        atomicMax(&out.stats[ST_BMAX], bmx);
-    }
-    if (lane == 0 && err) atomicOr(&out.stats[ST_ERROR], err);
+    const unsigned long long err = wave_or(st_err);
+    if (lane == 0) stats_atomics(out, sp, ss, smn, smx, sb, bmn, bmx, err);
 }
 
 template <bool COUNT, bool PROF>

@@ -55,23 +55,24 @@ hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const Rt
 __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long* counters,
                                   unsigned int* tile_counter) {
     const int t = threadIdx.x;
-    if (t < ST_WORDS) stats[t] = (t == ST_SMIN || t == ST_BMIN) ? ~0ull : 0ull;
+    if (t < ST_WORDS) stats[t * kStatStride] = (t == ST_SMIN || t == ST_BMIN) ? ~0ull : 0ull;
     if (counters && t < kCounterWords) counters[t] = 0ull;
     if (t == 0) *tile_counter = 0u;
 }
 
+constexpr int kAccBlock = 256;
 #ifndef RT_ACC_UNROLL
 #define RT_ACC_UNROLL 8
 #endif
 // Adds every pixel's samples in sample order (PixelStats.add), then
 // finalColor / u8 / RenderStats exactly as the sequential kernel.
-__global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
-                                                        SampleBuf sb) {
+__global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
+                                                              SampleBuf sb) {
     const RtCamera& C = S0.cam;
     const int lane = threadIdx.x & (kWave - 1);
-    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     PixStats st;
-    if (slot < sb.slots) {
+    // grid-stride over the pass's pixel slots: few blocks, one stats merge per block
+    for (int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < sb.slots; slot += gridDim.x * blockDim.x) {
         int i, j;
         item_pixel(reg, tiles_x, sb.tile0 + slot / 64, slot % 64, i, j);
         if (i < min(reg.x + reg.width, C.width) && j < min(reg.y + reg.height, C.height)) {
@@ -110,13 +111,35 @@ __global__ __launch_bounds__(256) void pt_accum_kernel(DevScene S0, RtRegion reg
             finish_pixel(C, out, opix, color, n, bsum, bmin, bmax, st);
         }
     }
-    publish_stats(out, st, 0ull, lane);
+    // RenderStats.merge: waves -> LDS -> one lane per block
+    __shared__ unsigned long long red[kAccBlock / kWave][7];
+    const int w = threadIdx.x / kWave;
+    const unsigned long long v[7] = {wave_sum(st.pixels), wave_sum(st.samples), wave_min(st.smin), wave_max(st.smax),
+                                     wave_sum(st.b),      wave_min(st.bmin),    wave_max(st.bmax)};
+    if (lane == 0)
+        for (int q = 0; q < 7; ++q) red[w][q] = v[q];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a[7];
+        for (int q = 0; q < 7; ++q) a[q] = red[0][q];
+        for (int u = 1; u < kAccBlock / kWave; ++u) {
+            a[0] += red[u][0];
+            a[1] += red[u][1];
+            a[2] = min(a[2], red[u][2]);
+            a[3] = max(a[3], red[u][3]);
+            a[4] += red[u][4];
+            a[5] = min(a[5], red[u][5]);
+            a[6] = max(a[6], red[u][6]);
+        }
+        stats_atomics(out, a[0], a[1], a[2], a[3], a[4], a[5], a[6], 0ull);
+    }
 }
 
 hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
                         const SampleBuf& sb, hipStream_t stream) {
-    const int grid = (sb.slots + 255) / 256;
-    hipLaunchKernelGGL(pt_accum_kernel, dim3(grid), dim3(256), 0, stream, S, reg, out, tiles_x, sb);
+    // about two blocks' worth of slots per thread-slot of the chip: 2 x 256 CUs x 1024 threads
+    const int grid = std::max(1, std::min((sb.slots + kAccBlock - 1) / kAccBlock, 2 * 256 * 1024 / kAccBlock));
+    hipLaunchKernelGGL(pt_accum_kernel, dim3(grid), dim3(kAccBlock), 0, stream, S, reg, out, tiles_x, sb);
     return hipGetLastError();
 }
 

@@ -182,7 +182,7 @@ struct rt_camera {
         append(blob, build.nodes, &off_nodes);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
         if (!blob.empty()) hip_check(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice), "hipMemcpy");
-        hip_check(hipMalloc(&d_stats, ST_WORDS * sizeof(unsigned long long)), "hipMalloc");
+        hip_check(hipMalloc(&d_stats, ST_WORDS * kStatStride * sizeof(unsigned long long)), "hipMalloc");
         hip_check(hipMalloc(&d_counters, kCounterWords * sizeof(unsigned long long)), "hipMalloc");
         hip_check(hipMalloc(&d_tile, 64), "hipMalloc");
         device = dev;
@@ -440,12 +440,13 @@ struct rt_camera {
     }
 
     void read_stats(rt_render_stats* st, uint64_t* counters, hipStream_t stream) {
-        unsigned long long w[ST_WORDS];
-        hip_check(hipMemcpyAsync(w, d_stats, sizeof w, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
+        unsigned long long wl[ST_WORDS * kStatStride], w[ST_WORDS];
+        hip_check(hipMemcpyAsync(wl, d_stats, sizeof wl, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
         unsigned long long c[kCounterWords];
         if (counters)
             hip_check(hipMemcpyAsync(c, d_counters, sizeof c, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
         hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        for (int k = 0; k < ST_WORDS; ++k) w[k] = wl[k * kStatStride];
         if (counters)
             for (int k = 0; k < kCounterWords; ++k) counters[k] = c[k];
         if (w[ST_ERROR] & ERR_NO_BACKGROUND)
