@@ -284,6 +284,13 @@ __device__ __forceinline__ bool box_hit(const RtNode& n, const RayK<Real>& r, Re
 template <class Real> __device__ __forceinline__ Real sphere_radius(const RtPrim& p);
 template <> __device__ __forceinline__ double sphere_radius<double>(const RtPrim& p) { return p.s0; }
 template <> __device__ __forceinline__ float sphere_radius<float>(const RtPrim& p) { return p.g0[3]; }
+// 1 / radius (Vec3.divide's reciprocal, vec3.ts:126-130), computed on the host with the same
+// IEEE division: sphere records carry it in g1 (double bits in g1[0..1], fp32 in g1[2]).
+template <class Real> __device__ __forceinline__ Real sphere_inv_radius(const RtPrim& p);
+template <> __device__ __forceinline__ double sphere_inv_radius<double>(const RtPrim& p) {
+    return __hiloint2double(__float_as_int(p.g1[1]), __float_as_int(p.g1[0]));
+}
+template <> __device__ __forceinline__ float sphere_inv_radius<float>(const RtPrim& p) { return p.g1[2]; }
 template <class Real> __device__ __forceinline__ Real plane_d(const RtPrim& p);
 template <> __device__ __forceinline__ double plane_d<double>(const RtPrim& p) { return p.s0; }
 template <> __device__ __forceinline__ float plane_d<float>(const RtPrim& p) { return p.g0[3]; }
@@ -1365,10 +1372,22 @@ __device__ __forceinline__ V3 light_generate(const DevScene& S, const RtLight& L
 }
 
 // CosinePDF.value (src/geometry/pdf.ts:43-46)
+// x / PI, correctly rounded: q = RN(x * RN(1/PI)) corrected once by the exact
+// residual x - q*PI (fma) - Markstein's theorem for a correctly rounded reciprocal
+// gives RN(x / PI) (also checked on 4e8 doubles in (0, 1], tools/probes/div_pi.c);
+// 3 fp64 operations instead of the division sequence.
+__device__ __forceinline__ double div_pi(double x) {
+    constexpr double kPi = 3.141592653589793, kInvPi = 1.0 / 3.141592653589793;
+    const double q = x * kInvPi;
+    const double r = __builtin_fma(-q, kPi, x);
+    return __builtin_fma(r, kInvPi, q);
+}
+__device__ __forceinline__ float div_pi(float x) { return x / K<float>::PI; }
+
 template <class Real>
 __device__ __forceinline__ Real cosine_value(const Onb& b, V3 dir) {
     const Real c = dot<Real>(unit<Real>(dir), b.w);
-    return c <= (Real)0 ? (Real)0 : c / K<Real>::PI;
+    return c <= (Real)0 ? (Real)0 : div_pi(c);
 }
 
 // writeColorToBuffer (src/camera.ts:455-472) into a Uint8ClampedArray.
@@ -1491,9 +1510,12 @@ struct Path {
 
 // Camera.getRay (src/camera.ts:176-210) for sample `sample` of pixel (i, j).
 // pixel00Loc + i*pixelDeltaU + j*pixelDeltaV (src/camera.ts:181), fixed per pixel.
+// The scalings by the integers i, j (< 2^16) are fp32 multiplies: an fp32 times an
+// integer below 2^24 is exact in double, so the double product rounded to fp32 is
+// the fp32 product (rt_math.hpp identities) - the ref build's result, bit for bit.
 template <class Real>
 __device__ __forceinline__ V3 pixel_center(const RtCamera& C, int i, int j) {
-    return add(add(ld3(C.pixel00), scale<Real>(ld3(C.du), (Real)i)), scale<Real>(ld3(C.dv), (Real)j));
+    return add(add(ld3(C.pixel00), scale<float>(ld3(C.du), (float)i)), scale<float>(ld3(C.dv), (float)j));
 }
 
 template <class Real, bool EMIT>
@@ -1586,7 +1608,7 @@ __device__ __forceinline__ int shade_hit(const DevScene& S, Path<EMIT>& P, int h
     p = ray_at<Real>(P.o, P.d, t);
     planar = pr.type != PRIM_SPHERE;
     if (!planar) {
-        nrm = divs<Real>(sub(p, ld3(pr.g0)), sphere_radius<Real>(pr));
+        nrm = scale<Real>(sub(p, ld3(pr.g0)), sphere_inv_radius<Real>(pr));  // Vec3.divide(radius)
         front = dot<Real>(P.d, nrm) <= (Real)0;
         if (!front) nrm = neg(nrm);
     } else {
@@ -1620,8 +1642,10 @@ __device__ __forceinline__ bool shade_diffuse(const DevScene& S, const RtCamera&
         b = make_onb<Real>(nrm);
     }
     const Real total = (Real)S.mix_total;
+    const bool total1 = S.mix_total == 1.0;  // x * 1 and x / 1 are exact: skip them (uniform branch)
     const Real lw = (Real)S.light_w;
-    const Real rnd = uniform<Real>(P.rng) * total;
+    const Real u0 = uniform<Real>(P.rng);
+    const Real rnd = total1 ? u0 : u0 * total;
     Real partial = (Real)0.5;
     V3 gdir;
     if (rnd < partial || C.n_lights == 0) {
@@ -1645,7 +1669,7 @@ __device__ __forceinline__ bool shade_diffuse(const DevScene& S, const RtCamera&
     Real sum = (Real)0.5 * cv;
     for (int l = 0; l < C.n_lights; ++l)
         sum += lw * light_pdf_value<Real, COUNT, true>(S, ld_uniform(S.glights, l), p, gdir, cnt);
-    const Real pv = sum / total;
+    const Real pv = total1 ? sum : sum / total;
     bool term = false;
     if (pv <= (Real)0.0001) {
         term = true;

@@ -722,6 +722,12 @@ struct Builder {
             double r = to_number(od.get("r"), NAN);
             p.s0 = r;
             p.g0[0] = c.x; p.g0[1] = c.y; p.g0[2] = c.z; p.g0[3] = (float)r;
+            {  // reciprocal radius for the hit normal (kernel sphere_inv_radius)
+                const double ir = 1.0 / r;
+                std::memcpy(&p.g1[0], &ir, sizeof ir);
+                const float irf = 1.0f / (float)r;
+                p.g1[2] = irf;
+            }
             V3 rv = mk<double>(r, r, r);
             box = Box{sub(c, rv), add(c, rv)};
             return p;
@@ -1111,10 +1117,13 @@ struct SahBuilder {
 // reference-order traversal.
 bool prims_inside_boxes(const std::vector<RtPrim>& prims) {
     for (const RtPrim& p : prims) {
-        for (int k = 0; k < 4; ++k)
-            if (std::isnan(p.g0[k]) || std::isnan(p.g1[k]) || std::isnan(p.g2[k]) || std::isnan(p.g3[k]) ||
-                std::isnan(p.g4[k]))
+        for (int k = 0; k < 4; ++k) {
+            if (std::isnan(p.g0[k])) return false;
+            // a sphere's g1 holds its reciprocal radius (double bits), its g2..g4 are unused
+            if (p.type != PRIM_SPHERE &&
+                (std::isnan(p.g1[k]) || std::isnan(p.g2[k]) || std::isnan(p.g3[k]) || std::isnan(p.g4[k])))
                 return false;
+        }
         if (std::isnan(p.s0)) return false;
         if (p.type == PRIM_SPHERE) {
             if (!(p.s0 > 0) || !std::isfinite(p.s0)) return false;
