@@ -2039,6 +2039,22 @@ __device__ __forceinline__ void item_decode(const SampleBuf& sb, const PhaseRow*
     s_end = s + r.chunk;
 }
 
+// Item hand-out: every wave's first pool is static (wave w takes items
+// [w * pool, (w + 1) * pool)), the global counter deals the rest from
+// grid_waves * pool on - so the launch does not open with every wave's atomic
+// on one word (4096 returning atomics serialise for ~50 us).
+__device__ __forceinline__ void first_pool(const SampleBuf& sb, int& pool_next, int& pool_end, bool& exhausted) {
+    const int gw = (int)(blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave);
+    pool_next = gw * sb.pool;
+    pool_end = min(pool_next + sb.pool, sb.n_items);
+    exhausted = pool_next >= sb.n_items;
+}
+__device__ __forceinline__ int take_pool(const RenderOut& out, const SampleBuf& sb, int lane) {
+    int base = 0;
+    if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
+    return __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64)) + (int)(gridDim.x * (blockDim.x / kWave)) * sb.pool;
+}
+
 template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
 __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRegion reg, RenderOut out,
                                                                         int tiles_x, SampleBuf sb) {
@@ -2066,8 +2082,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     Prof pf;
     prof_init<PROF>(pf, prof_lds, lane);
 
-    int pool_next = 0, pool_end = 0;  // wave-uniform
-    bool exhausted = false;           // wave-uniform
+    int pool_next, pool_end;  // wave-uniform
+    bool exhausted;           // wave-uniform
+    first_pool(sb, pool_next, pool_end, exhausted);
     int slot = -1;                    // this lane's pixel slot (-1: idle)
     int s = 0, s_end = 0, i = 0, j = 0;
     uint32_t pix = 0;
@@ -2087,9 +2104,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
         const int n_need = __popcll(need);
         if (n_need != 0 && !exhausted && (n_need >= sb.refill_min || __ballot(slot >= 0) == 0ull)) {
             if (pool_next >= pool_end) {
-                int base = 0;
-                if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
-                base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+                const int base = take_pool(out, sb, lane);
                 if (base >= n_items) {
                     exhausted = true;
                 } else {
@@ -2269,8 +2284,9 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
         G[k] = make_float4(0.f, 0.f, __int_as_float(PH_ITEM), 0.f);
     }
     int a_head = 0, a_cnt = kPoolK, d_head = 0, d_cnt = 0;  // wave-uniform queue state
-    int pool_next = 0, pool_end = 0;                       // wave-uniform item hand-out
-    bool exhausted = false;
+    int pool_next, pool_end;  // wave-uniform item hand-out
+    bool exhausted;
+    first_pool(sb, pool_next, pool_end, exhausted);
 
     // the sample's radiance and bounce count to its record; the slot's next phase
     auto record = [&](V3 c, int bounces, int slot, int& s, int s_end) -> int {
@@ -2341,9 +2357,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
             const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
             if (need != 0ull && !exhausted) {
                 if (pool_next >= pool_end) {
-                    int base = 0;
-                    if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
-                    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+                    const int base = take_pool(out, sb, lane);
                     if (base >= n_items) {
                         exhausted = true;
                     } else {

@@ -402,7 +402,7 @@ struct rt_camera {
                 sb.item_base[p] = (int32_t)items;
                 items += (long)sb.slots * sb.nch[p];
             }
-            if (items >= (1l << 31) - 4096) throw std::runtime_error("chunked pass too large");
+            if (items >= (1l << 31) - (1l << 22)) throw std::runtime_error("chunked pass too large");  // counter headroom: 2 x grid waves x pool
             sb.n_items = (int32_t)items;
             if (t0 > 0) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = g;
