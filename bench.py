@@ -44,6 +44,12 @@ SCENES = {
 }
 
 
+KERNEL_DESC = {
+    "pool": "stage-compacted pool (per-wave LDS path slots, trace/diffuse queues, in-order accumulate)",
+    "chunked": "chunked (lane work pool, in-order accumulate)",
+}
+
+
 def log(msg: str) -> None:
     """Progress on stderr (long runs must keep writing)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -192,7 +198,7 @@ def roofline(cfg_key: str, build: str, samples: int, kernel_ms: float, counters,
         out.update({"achieved": round(ach, 2), "frac": round(ach / VALU_PEAK_GINST, 4),
                     "lane_util": v["lane_util"], "useful_lane_frac": round(ach / VALU_PEAK_GINST * v["lane_util"], 4),
                     "valu_wave_insts_per_sample": round(ips, 2),
-                    "kernel": v["kernel"], "pmc_build": v.get("build_id"), "pmc_stale": v.get("build_id") != build,
+                    "pmc_kernel": v["kernel"], "pmc_build": v.get("build_id"), "pmc_stale": v.get("build_id") != build,
                     "pmc_source": "profiles/pmc_valu.json"})
         assert out["frac"] <= 1.0, out
     else:
@@ -324,7 +330,8 @@ def main(argv=None):
     passes = cam.pass_count()
     kernel_ms = sum(a for a, _ in kt) / len(kt)
     accum_ms = sum(b for _, b in kt) / len(kt)
-    kernel_name = "pt_chunk_kernel" if accum_ms > 0 else "pt_render_kernel"
+    kind = cam.last_kernel()  # the path kernel the library launched (rt_camera_last_kernel)
+    kernel_name = {"pool": "pt_pool_kernel", "chunked": "pt_chunk_kernel"}.get(kind, "pt_render_kernel")
 
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
@@ -365,8 +372,7 @@ def main(argv=None):
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "depth": args.depth,
                        "precision": args.precision, "adaptive": False,
                        "traversal": ["fast", "reference", "brute"][cam.info["traversal"]],
-                       "kernel": "chunked (lane work pool, in-order accumulate)" if accum_ms > 0
-                                 else "sequential (wave per 8x8 tile)",
+                       "kernel": KERNEL_DESC.get(kind, "sequential (wave per 8x8 tile)"),
                        "parallelism": f"8x8-tile interleave x{world}" +
                                       (" + RCCL gather of tile-packed slabs to rank 0" if world > 1 else "")},
             "build_id": rt.build_id(),
