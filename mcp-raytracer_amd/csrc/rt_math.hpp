@@ -13,7 +13,9 @@
 //    equals the fp32 operation (double has > 2*24+2 bits), so vec+vec, vec-vec
 //    and vec*vec (gl-matrix add/subtract/multiply) are done directly in fp32.
 //  * products of two fp32 values are exact in double, so dot products only
-//    round in the two additions, exactly like `a[0]*b[0] + a[1]*b[1] + a[2]*b[2]`.
+//    round in the two additions, exactly like `a[0]*b[0] + a[1]*b[1] + a[2]*b[2]`,
+//    and an fma whose product term is such a product rounds exactly as the
+//    reference's separate multiply and add (dot, cross).
 #pragma once
 
 #include <cmath>
@@ -55,25 +57,39 @@ template <class Real>
 RT_HD V3 divs(V3 a, Real t) { return scale<Real>(a, (Real)1 / t); }
 
 // Vec3.dot / lengthSquared (src/geometry/vec3.ts:132-136,152-157).
+// In double each product of two fp32 values is exact, so fma(y1, y2, x1*x2) =
+// RN(x1*x2 + y1*y2) is the reference's rounded sum, bit for bit (signed zeros
+// and NaN/inf propagation included): 3 fp64 operations instead of 5.
 template <class Real>
 RT_HD Real dot(V3 a, V3 b) {
-    return (Real)a.x * (Real)b.x + (Real)a.y * (Real)b.y + (Real)a.z * (Real)b.z;
+    if constexpr (sizeof(Real) == 8)
+        return __builtin_fma((double)a.z, (double)b.z,
+                             __builtin_fma((double)a.y, (double)b.y, (double)a.x * (double)b.x));
+    else
+        return (Real)a.x * (Real)b.x + (Real)a.y * (Real)b.y + (Real)a.z * (Real)b.z;
 }
 template <class Real>
 RT_HD Real len2(V3 a) { return dot<Real>(a, a); }
 
 // gl-matrix vec3.cross: each component formed in double, rounded to fp32.
+// Each component x1*y2 - x2*y1 of exact double products = fma(x1, y2, -(x2*y1)).
+template <class Real>
+RT_HD Real xmul_sub(float x1, float y2, float x2, float y1) {
+    if constexpr (sizeof(Real) == 8)
+        return __builtin_fma((double)x1, (double)y2, -((double)x2 * (double)y1));
+    else
+        return (Real)x1 * (Real)y2 - (Real)x2 * (Real)y1;
+}
 template <class Real>
 RT_HD V3 cross(V3 a, V3 b) {
-    return V3{(float)((Real)a.y * (Real)b.z - (Real)a.z * (Real)b.y),
-              (float)((Real)a.z * (Real)b.x - (Real)a.x * (Real)b.z),
-              (float)((Real)a.x * (Real)b.y - (Real)a.y * (Real)b.x)};
+    return V3{(float)xmul_sub<Real>(a.y, b.z, a.z, b.y), (float)xmul_sub<Real>(a.z, b.x, a.x, b.z),
+              (float)xmul_sub<Real>(a.x, b.y, a.y, b.x)};
 }
 
 // gl-matrix 3.4.3 vec3.normalize: len = x²+y²+z²; if (len > 0) len = 1/sqrt(len).
 template <class Real>
 RT_HD V3 unit(V3 a) {
-    Real l = (Real)a.x * (Real)a.x + (Real)a.y * (Real)a.y + (Real)a.z * (Real)a.z;
+    Real l = dot<Real>(a, a);
     if (l > (Real)0) l = (Real)1 / sqrt(l);
     return V3{(float)((Real)a.x * l), (float)((Real)a.y * l), (float)((Real)a.z * l)};
 }
