@@ -2221,8 +2221,13 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 // appends): D once 64 paths wait (or when it is the longer queue), A
 // otherwise. So the diffuse shading runs on full waves rather than on the
 // lanes whose path happens to need it in a given trip (the north star's
-// persistent-wavefront work queues). Each path's arithmetic and draw order are
-// path_trip's, so every sample record - and the image - is bit-identical.
+// persistent-wavefront work queues). D is split by the mixture's branch
+// (RT_POOL_DSPLIT): A draws the mixture uniform ahead (on a copy of the path's
+// RNG state; D draws the same value again) and queues the path for the
+// cosine-PDF or the light-PDF generate, so a D trip runs one of the two
+// sampling branches instead of both at half the lanes. Each path's arithmetic
+// and draw order are path_trip's, so every sample record - and the image - is
+// bit-identical.
 // ---------------------------------------------------------------------------
 #ifndef RT_POOL_K
 #define RT_POOL_K 96
@@ -2230,11 +2235,16 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 #ifndef RT_POOL_BLOCK
 #define RT_POOL_BLOCK 1024
 #endif
+#ifndef RT_POOL_DSPLIT
+#define RT_POOL_DSPLIT 1
+#endif
 constexpr int kPoolK = RT_POOL_K;          // path slots per wave
 constexpr int kBlockPool = RT_POOL_BLOCK;  // persistent workgroup size
 constexpr int kPoolGroups = 5;             // 16-byte groups per slot (below)
 static_assert(kPoolK >= kWave && kPoolK <= 256, "pool slots: one full wave, u8 queue entries");
-// Per wave: slot state as [group][slot] float4, then the A and D queues (u8 slot indices).
+// Per wave: slot state as [group][slot] float4, then the A queue (a ring) and the D queue
+// (u8 slot indices; with RT_POOL_DSPLIT two stacks in one array: cosine-branch paths from
+// the bottom, light-branch paths from the top - together at most kPoolK entries).
 //   g0 {rng lo, rng hi, phase, s_end}  phase: bounces so far (>= 0), PH_NEW or PH_ITEM
 //   g1 {o (hit point p when queued for D), slot}
 //   g2 {d (the face normal when queued for D), s}
@@ -2252,6 +2262,16 @@ __device__ __forceinline__ void queue_push(uint8_t* q, int head, int& cnt, bool 
     if (want) {
         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         q[pool_ring(pool_ring(head + cnt) + r)] = (uint8_t)k;
+    }
+    cnt += __popcll(m);
+}
+
+// Stacks in one array: the bottom one fills [0, cnt), the top one [kPoolK - cnt, kPoolK).
+__device__ __forceinline__ void stack_push(uint8_t* q, bool top, int& cnt, bool want, int k) {
+    const unsigned long long m = __ballot(want);
+    if (want) {
+        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        q[top ? kPoolK - 1 - (cnt + r) : cnt + r] = (uint8_t)k;
     }
     cnt += __popcll(m);
 }
@@ -2284,6 +2304,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
         G[k] = make_float4(0.f, 0.f, __int_as_float(PH_ITEM), 0.f);
     }
     int a_head = 0, a_cnt = kPoolK, d_head = 0, d_cnt = 0;  // wave-uniform queue state
+    int dl_cnt = 0;  // RT_POOL_DSPLIT: light-branch stack (d_cnt: cosine-branch stack)
     int pool_next, pool_end;  // wave-uniform item hand-out
     bool exhausted;
     first_pool(sb, pool_next, pool_end, exhausted);
@@ -2300,15 +2321,24 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
         return s < s_end ? PH_NEW : PH_ITEM;
     };
 
-    while (a_cnt + d_cnt > 0) {
+    while (a_cnt + d_cnt + dl_cnt > 0) {
         // other lanes' slot and queue writes of the previous trip (one wave: LDS is in order)
         __asm__ volatile("" ::: "memory");
-        if (d_cnt >= kWave || d_cnt > a_cnt) {
+        const bool dtop = RT_POOL_DSPLIT && dl_cnt > d_cnt;  // the longer D stack
+        const int dn = dtop ? dl_cnt : d_cnt;
+        if (dn >= kWave || dn > a_cnt) {
             // ---- D: diffuse shading of up to 64 queued paths ----
-            const int n = min(kWave, d_cnt);
-            const int k = lane < n ? (int)qd[pool_ring(d_head + lane)] : -1;
-            d_head = pool_ring(d_head + n);
-            d_cnt -= n;
+            const int n = min(kWave, dn);
+            int k = -1;
+            if (RT_POOL_DSPLIT) {
+                if (lane < n) k = (int)qd[dtop ? kPoolK - dl_cnt + lane : d_cnt - n + lane];
+                if (dtop) dl_cnt -= n;
+                else d_cnt -= n;
+            } else {
+                if (lane < n) k = (int)qd[pool_ring(d_head + lane)];
+                d_head = pool_ring(d_head + n);
+                d_cnt -= n;
+            }
             if (k >= 0) {
                 const float4 g0 = G[k], g1 = G[kPoolK + k], g2 = G[2 * kPoolK + k], g3 = G[3 * kPoolK + k],
                              g4 = G[4 * kPoolK + k];
@@ -2385,7 +2415,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 }
             }
             const bool keep = k >= 0 && (phase != PH_ITEM || !exhausted);  // drained slots leave the pool
-            bool to_d = false;
+            bool to_d = false, d_light = false;
             if (k >= 0 && phase != PH_ITEM) {
                 const RtCamera& C = cam_opaque();
                 Path<false> P;
@@ -2430,6 +2460,12 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                                 to_d = true;
                                 P.d = nrm;  // queued for D: g2 carries the face normal
                                 hf = h | (planar ? (1 << 30) : 0) | (front ? (int)0x80000000 : 0);
+                                if (RT_POOL_DSPLIT) {  // shade_diffuse's first draw and branch, ahead
+                                    uint64_t r = P.rng;
+                                    const Real u0 = uniform<Real>(r);
+                                    const Real rnd = S.mix_total == 1.0 ? u0 : u0 * (Real)S.mix_total;
+                                    d_light = !(rnd < (Real)0.5 || C.n_lights == 0);
+                                }
                             }
                         }
                     }
@@ -2449,7 +2485,12 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 G[3 * kPoolK + k] = g3;
             }
             queue_push(qa, a_head, a_cnt, keep && !to_d, k);
-            queue_push(qd, d_head, d_cnt, to_d, k);
+            if (RT_POOL_DSPLIT) {
+                stack_push(qd, false, d_cnt, to_d && !d_light, k);
+                stack_push(qd, true, dl_cnt, to_d && d_light, k);
+            } else {
+                queue_push(qd, d_head, d_cnt, to_d, k);
+            }
         }
     }
     PixStats st;
