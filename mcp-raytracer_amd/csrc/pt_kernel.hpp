@@ -39,6 +39,7 @@ struct DevScene {
     const RtTNode* __restrict__ tnodes; // fast traversal: children-in-parent nodes (blob start)
     const RtPrim* __restrict__ prims;   // global, or LDS in an LDS-resident launch
     const RtPrim* __restrict__ gprims;  // always the global copy (scalar-load reads)
+    const RtPre* __restrict__ gpre;     // brute-force pre-filter records (global, scalar-load reads)
     const int32_t* __restrict__ tprims; // fast-traversal leaves -> primitive slots (LDS when resident)
     const float4* __restrict__ tsph;    // per tprims entry: sphere {centre, fp32 radius} or NaNs (LDS when resident)
     const RtMat* __restrict__ mats;
@@ -376,32 +377,38 @@ __device__ __forceinline__ bool aquad_t_c(const RtPrim& p, V3 o3, V3 d3, Real tm
 // fp32 pre-filter of aquad_t_c: false only when the exact test surely rejects or
 // gives no t <= thi.
 // `lo` (all pre-filters): a lower bound of the exact t the test can return.
+// Fields: na = n[a], D, q1 = Q[ia], q2 = Q[ib], sw = +-w[a], sv = v[iv], su = u[iu] (RtPre order).
 template <int CODE>
-__device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, const float* d, float dn, float thi,
-                                              float& lo) {
+__device__ __forceinline__ bool aquad_maybe_v(float na, float D, float q1, float q2, float sw, float sv, float su,
+                                              const float* o, const float* d, float dn, float thi, float& lo) {
     constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
     constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
-    const float na = p.g3[a];
     const float denom = na * d[a];
     lo = kTminLo;
     if (!(::fabsf(denom) > 1e-3f * dn)) return true;  // near-parallel: decide exactly
     const float no = na * o[a];
-    const float D = p.g0[3];
     const float idn = __builtin_amdgcn_rcpf(denom);
     const float t = (D - no) * idn;
     const float et = kRel * ((::fabsf(D) + ::fabsf(no)) * ::fabsf(idn) + 2.0f * ::fabsf(t)) + 1e-30f;
     if (t + et < kTminLo || t - et > thi) return false;
     lo = t - et;
-    const float ph1 = o[ia] + t * d[ia] - p.g0[ia];
-    const float ph2 = o[ib] + t * d[ib] - p.g0[ib];
-    const float alpha = p.g3[3] * (ph1 * p.g2[3]);
-    const float beta = p.g3[3] * (ph2 * p.g1[3]);
+    const float ph1 = o[ia] + t * d[ia] - q1;
+    const float ph2 = o[ib] + t * d[ib] - q2;
+    const float alpha = sw * (ph1 * sv);
+    const float beta = sw * (ph2 * su);
     // in-plane hit-point error, times |w_a v| (alpha) / |w_a u| (beta)
-    const float dp1 = et * ::fabsf(d[ia]) + kRel * (::fabsf(o[ia]) + ::fabsf(t * d[ia]) + ::fabsf(p.g0[ia]));
-    const float dp2 = et * ::fabsf(d[ib]) + kRel * (::fabsf(o[ib]) + ::fabsf(t * d[ib]) + ::fabsf(p.g0[ib]));
-    const float ea = ::fabsf(p.g3[3] * p.g2[3]) * dp1 + 1e-4f;
-    const float eb = ::fabsf(p.g3[3] * p.g1[3]) * dp2 + 1e-4f;
+    const float dp1 = et * ::fabsf(d[ia]) + kRel * (::fabsf(o[ia]) + ::fabsf(t * d[ia]) + ::fabsf(q1));
+    const float dp2 = et * ::fabsf(d[ib]) + kRel * (::fabsf(o[ib]) + ::fabsf(t * d[ib]) + ::fabsf(q2));
+    const float ea = ::fabsf(sw * sv) * dp1 + 1e-4f;
+    const float eb = ::fabsf(sw * su) * dp2 + 1e-4f;
     return !(alpha < -ea || alpha > 1.0f + ea || beta < -eb || beta > 1.0f + eb);
+}
+template <int CODE>
+__device__ __forceinline__ bool aquad_maybe_c(const RtPrim& p, const float* o, const float* d, float dn, float thi,
+                                              float& lo) {
+    constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
+    constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+    return aquad_maybe_v<CODE>(p.g3[a], p.g0[3], p.g0[ia], p.g0[ib], p.g3[3], p.g2[3], p.g1[3], o, d, dn, thi, lo);
 }
 
 template <class Real>
@@ -1168,15 +1175,98 @@ __device__ __forceinline__ bool prim_exact(const RtPrim& p, const RayK<Real>& r,
     return planar_t<Real, false>(p, r, K<Real>::TMIN, inf, t);
 }
 
+// prim_exact with the sphere's root and the axis-aligned quad's plane t through ONE
+// division: lanes of a wave test different primitive types, and each type's block
+// costs the whole wave; the prologues stay per type, the division (the longest
+// piece of either) is shared. Same operations on the same operands: sphere_t's
+// (-h - sqrt(disc)) / a and aquad_t_rt's (D - n.o) / (n.d).
+#ifndef RT_NF_FUSED
+#define RT_NF_FUSED 1
+#endif
+template <class Real>
+__device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Real>& r, Real& t) {
+    const Real inf = (Real)__builtin_inf();
+    const int code = aquad_code(p);
+    const bool sph = p.type == PRIM_SPHERE;
+    if (!sph && !(p.type == PRIM_QUAD && code != 0)) return prim_exact<Real>(p, r, t);
+    Real num, den, halfB = (Real)0, sq = (Real)0;
+    float o1 = 0.f, d1 = 0.f, o2 = 0.f, d2 = 0.f, q1 = 0.f, q2 = 0.f;
+    if (sph) {
+        const V3 c = ld3(p.g0);
+        const Real rad = sphere_radius<Real>(p);
+        const V3 oc = sub(r.o, c);
+        halfB = dot<Real>(oc, r.d);
+        const Real cc = len2<Real>(oc) - rad * rad;
+        const Real disc = halfB * halfB - r.a * cc;
+        if (disc < (Real)0) return false;
+        sq = m_sqrt(disc);
+        num = -halfB - sq;
+        den = r.a;
+    } else {
+        const int a = (int)((aquad_axes(0) >> (2 * code)) & 3u);
+        const int ia = (int)((aquad_axes(1) >> (2 * code)) & 3u);
+        const int ib = (int)((aquad_axes(2) >> (2 * code)) & 3u);
+        const V3 o3 = r.o, d3 = r.d;
+        const float oa = sel3(o3.x, o3.y, o3.z, a), da = sel3(d3.x, d3.y, d3.z, a);
+        o1 = sel3(o3.x, o3.y, o3.z, ia);
+        d1 = sel3(d3.x, d3.y, d3.z, ia);
+        o2 = sel3(o3.x, o3.y, o3.z, ib);
+        d2 = sel3(d3.x, d3.y, d3.z, ib);
+        q1 = sel3(p.g0[0], p.g0[1], p.g0[2], ia);
+        q2 = sel3(p.g0[0], p.g0[1], p.g0[2], ib);
+        if (!(::isfinite(o1) && ::isfinite(d1) && ::isfinite(o2) && ::isfinite(d2))) return false;
+        const Real na = (Real)sel3(p.g3[0], p.g3[1], p.g3[2], a);
+        den = na * (Real)da;
+        if (m_abs(den) < (Real)1e-8) return false;
+        num = plane_d<Real>(p) - na * (Real)oa;
+    }
+    Real q = num / den;
+    if (sph) {
+        if (!(K<Real>::TMIN < q && q < inf)) {
+            q = (-halfB + sq) / r.a;
+            if (!(K<Real>::TMIN < q && q < inf)) return false;
+        }
+    } else {
+        if (!(K<Real>::TMIN < q && q < inf)) return false;
+        const float ph1 = (o1 + (float)((Real)d1 * q)) - q1;
+        const float ph2 = (o2 + (float)((Real)d2 * q)) - q2;
+        const Real sw = (Real)p.g3[3];
+        const Real alpha = sw * (Real)(ph1 * p.g2[3]);
+        const Real beta = sw * (Real)(ph2 * p.g1[3]);
+        if (alpha < (Real)0 || alpha > (Real)1 || beta < (Real)0 || beta > (Real)1) return false;
+    }
+    t = q;
+    return true;
+}
+
 template <class Real, bool COUNT>
 __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
                                                     float* lot, uint32_t* cnt) {
     const FRay f = make_fray(r.o, r.d);
     uint32_t mask = 0u;
     for (int k = 0; k < n_prims; ++k) {
-        const RtPrim p = ld_uniform(S.gprims, k);
+        const RtPre q = ld_uniform(S.gpre, k);  // one scalar load (wave-uniform)
         float lo;
-        if (prim_maybe<COUNT>(p, f, lo, cnt)) {
+        bool maybe;
+        if (q.kind == PRE_SPHERE) {
+            if (COUNT) cnt[CT_SPHERE]++;
+            maybe = sphere_maybe(make_float4(q.f[0], q.f[1], q.f[2], q.f[3]), f, __builtin_inff(), lo);
+        } else if (q.kind != PRE_OTHER) {
+            if (COUNT) cnt[CT_QUAD]++;
+            const float* v = q.f;
+            const float inf = __builtin_inff();
+            switch (q.kind) {
+                case 1: maybe = aquad_maybe_v<1>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
+                case 2: maybe = aquad_maybe_v<2>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
+                case 3: maybe = aquad_maybe_v<3>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
+                case 4: maybe = aquad_maybe_v<4>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
+                case 5: maybe = aquad_maybe_v<5>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
+                default: maybe = aquad_maybe_v<6>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
+            }
+        } else {
+            maybe = prim_maybe<COUNT>(ld_uniform(S.gprims, k), f, lo, cnt);
+        }
+        if (maybe) {
             lot[k * kStackStride] = lo;
             mask |= 1u << k;
         }
@@ -1200,7 +1290,9 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
         mask &= ~(1u << kb);
         if (COUNT) count_exact(cnt);
         Real t;
-        if (prim_exact<Real>(S.prims[kb], ray_at_use<Real>(r), t) && (t < best_t || (t == best_t && kb < best))) {
+        const bool hit = RT_NF_FUSED ? prim_exact_fused<Real>(S.prims[kb], ray_at_use<Real>(r), t)
+                                     : prim_exact<Real>(S.prims[kb], ray_at_use<Real>(r), t);
+        if (hit && (t < best_t || (t == best_t && kb < best))) {
             best_t = t;
             best = kb;
             thi = upper_f<Real>(t);

@@ -111,6 +111,7 @@ struct rt_camera {
     int32_t lds_words = 0;    // [tnodes][tprims][tsph][prims] prefix, 16-byte words
     int32_t lds_words2 = 0;   // the same + [mats][lights]
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
+    int32_t off_pre = 0;
     int32_t n_onb = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     // HIP events of the last launch, 3 per pass: path kernel start, path kernel
@@ -154,6 +155,37 @@ struct rt_camera {
         device = -1;
     }
 
+    // RtPre (scene.hpp) of every primitive, from its RtPrim fields
+    static std::vector<RtPre> prefilter_records(const std::vector<RtPrim>& prims) {
+        std::vector<RtPre> out(prims.size());
+        for (size_t k = 0; k < prims.size(); ++k) {
+            const RtPrim& p = prims[k];
+            RtPre q{};
+            int32_t code = 0;
+            std::memcpy(&code, &p.g4[3], sizeof code);
+            if (p.type == PRIM_SPHERE) {
+                q.kind = PRE_SPHERE;
+                for (int i = 0; i < 4; ++i) q.f[i] = p.g0[i];
+            } else if (p.type == PRIM_QUAD && code >= 1 && code <= 6) {
+                const int a = (code - 1) % 3, vflag = (code - 1) / 3;
+                const int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+                q.kind = code;
+                q.f[0] = p.g3[a];
+                q.f[1] = p.g0[3];
+                q.f[2] = p.g0[ia];
+                q.f[3] = p.g0[ib];
+                q.f[4] = p.g3[3];
+                q.f[5] = p.g2[3];
+                q.f[6] = p.g1[3];
+            } else {
+                q.kind = PRE_OTHER;
+            }
+            out[k] = q;
+        }
+        if (out.empty()) out.resize(1);  // 16-byte multiple, never empty
+        return out;
+    }
+
     template <class T>
     static void append(std::vector<char>& blob, const std::vector<T>& v, int32_t* off) {
         if ((v.size() * sizeof(T)) % 16) throw std::runtime_error("blob sections must be 16-byte multiples");
@@ -180,6 +212,7 @@ struct rt_camera {
         append(blob, onbs, &off_onbs);
         lds_words2 = (int32_t)(blob.size() / 16);
         append(blob, build.nodes, &off_nodes);
+        append(blob, prefilter_records(build.prims), &off_pre);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
         if (!blob.empty()) hip_check(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice), "hipMemcpy");
         hip_check(hipMalloc(&d_stats, ST_WORDS * kStatStride * sizeof(unsigned long long)), "hipMalloc");
@@ -223,6 +256,7 @@ struct rt_camera {
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.prims = reinterpret_cast<const RtPrim*>(b + off_prims);
         S.gprims = S.prims;
+        S.gpre = reinterpret_cast<const RtPre*>(b + off_pre);
         S.tprims = reinterpret_cast<const int32_t*>(b + off_tprims);
         S.off_tprims = off_tprims;
         S.tsph = reinterpret_cast<const float4*>(b + off_tsph);
