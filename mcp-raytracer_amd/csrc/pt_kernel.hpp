@@ -2330,6 +2330,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 #ifndef RT_POOL_DSPLIT
 #define RT_POOL_DSPLIT 1
 #endif
+#ifndef RT_POOL_ASPLIT
+#define RT_POOL_ASPLIT 1  // A queue split: paths to start (and slots needing an item) | paths in flight
+#endif
 constexpr int kPoolK = RT_POOL_K;          // path slots per wave
 constexpr int kBlockPool = RT_POOL_BLOCK;  // persistent workgroup size
 constexpr int kPoolGroups = 5;             // 16-byte groups per slot (below)
@@ -2397,6 +2400,9 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     }
     int a_head = 0, a_cnt = kPoolK, d_head = 0, d_cnt = 0;  // wave-uniform queue state
     int dl_cnt = 0;  // RT_POOL_DSPLIT: light-branch stack (d_cnt: cosine-branch stack)
+    // RT_POOL_ASPLIT: the A queue as two stacks in qa: paths to start from the bottom (an_cnt),
+    // paths in flight from the top (ac_cnt); a_cnt stays their sum
+    int an_cnt = kPoolK, ac_cnt = 0;
     int pool_next, pool_end;  // wave-uniform item hand-out
     bool exhausted;
     first_pool(sb, pool_next, pool_end, exhausted);
@@ -2418,10 +2424,12 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
         __asm__ volatile("" ::: "memory");
         const bool dtop = RT_POOL_DSPLIT && dl_cnt > d_cnt;  // the longer D stack
         const int dn = dtop ? dl_cnt : d_cnt;
-        if (dn >= kWave || dn > a_cnt) {
+        const bool atop = RT_POOL_ASPLIT && ac_cnt > an_cnt;  // the longer A stack
+        const int an = RT_POOL_ASPLIT ? (atop ? ac_cnt : an_cnt) : a_cnt;
+        if (dn >= kWave || dn > an) {
             // ---- D: diffuse shading of up to 64 queued paths ----
             const int n = min(kWave, dn);
-            int k = -1;
+            int k = -1, phase = 0;
             if (RT_POOL_DSPLIT) {
                 if (lane < n) k = (int)qd[dtop ? kPoolK - dl_cnt + lane : d_cnt - n + lane];
                 if (dtop) dl_cnt -= n;
@@ -2445,7 +2453,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 const int h = hf & 0x3fffffff;
                 const int s_end = __float_as_int(g0.w), slot = __float_as_int(g1.w);
                 int s = __float_as_int(g2.w);
-                int phase = P.bounces;
+                phase = P.bounces;
                 const RtCamera& C = cam_opaque();
                 if (shade_diffuse<Real, false, false, false>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
                                                              V3{g4.x, g4.y, g4.z}, cnt, pf)) {
@@ -2459,13 +2467,27 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 G[2 * kPoolK + k] = make_float4(P.d.x, P.d.y, P.d.z, __int_as_float(s));
                 G[3 * kPoolK + k] = make_float4(P.T.x, P.T.y, P.T.z, g3.w);
             }
-            queue_push(qa, a_head, a_cnt, k >= 0, k);
+            if (RT_POOL_ASPLIT) {
+                stack_push(qa, false, an_cnt, k >= 0 && phase < 0, k);
+                stack_push(qa, true, ac_cnt, k >= 0 && phase >= 0, k);
+                a_cnt = an_cnt + ac_cnt;
+            } else {
+                queue_push(qa, a_head, a_cnt, k >= 0, k);
+            }
         } else {
             // ---- A: trace up to 64 queued paths ----
-            const int n = min(kWave, a_cnt);
-            const int k = lane < n ? (int)qa[pool_ring(a_head + lane)] : -1;
-            a_head = pool_ring(a_head + n);
-            a_cnt -= n;
+            const int n = min(kWave, an);
+            int k = -1;
+            if (RT_POOL_ASPLIT) {
+                if (lane < n) k = (int)qa[atop ? kPoolK - ac_cnt + lane : an_cnt - n + lane];
+                if (atop) ac_cnt -= n;
+                else an_cnt -= n;
+                a_cnt -= n;
+            } else {
+                if (lane < n) k = (int)qa[pool_ring(a_head + lane)];
+                a_head = pool_ring(a_head + n);
+                a_cnt -= n;
+            }
             float4 g0 = make_float4(0.f, 0.f, __int_as_float(PH_ITEM), 0.f), g1 = g0, g2 = g0, g3 = g0;
             if (k >= 0) {
                 g0 = G[k];
@@ -2576,7 +2598,13 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 G[2 * kPoolK + k] = g2;
                 G[3 * kPoolK + k] = g3;
             }
-            queue_push(qa, a_head, a_cnt, keep && !to_d, k);
+            if (RT_POOL_ASPLIT) {
+                stack_push(qa, false, an_cnt, keep && !to_d && phase < 0, k);
+                stack_push(qa, true, ac_cnt, keep && !to_d && phase >= 0, k);
+                a_cnt = an_cnt + ac_cnt;
+            } else {
+                queue_push(qa, a_head, a_cnt, keep && !to_d, k);
+            }
             if (RT_POOL_DSPLIT) {
                 stack_push(qd, false, d_cnt, to_d && !d_light, k);
                 stack_push(qd, true, dl_cnt, to_d && d_light, k);
