@@ -78,6 +78,9 @@ enum {
     CT_BOUNCES, CT_DIFFUSE, CT_SAMPLES, CT_RAYS,
     CT_EXACT,       // primitives whose exact fp64 test ran (per lane)
     CT_EXACT_WAVE,  // exact-test blocks a wave executed (any lane), counted once per wave
+    CT_CAND0,       // brute force: rays with no pre-filter candidate
+    CT_CAND2,       // brute force: rays with two or more pre-filter candidates
+    CT_EXACT2,      // brute force: rays that needed two or more exact tests
     CT_WORDS
 };
 enum : unsigned long long { ERR_NO_BACKGROUND = 1ull, ERR_EMIT_STACK = 2ull };
@@ -1274,6 +1277,11 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
     Real best_t = (Real)__builtin_inf();
     int best = -1;
     float thi = __builtin_inff();
+    int n_exact = 0;
+    if (COUNT) {
+        cnt[CT_CAND0] += mask == 0u ? 1u : 0u;
+        cnt[CT_CAND2] += __popc(mask) >= 2 ? 1u : 0u;
+    }
     while (mask != 0u) {
         // nearest remaining candidate (a NaN bound is never skipped: it is tested exactly)
         int kb = __builtin_ctz(mask);
@@ -1288,7 +1296,10 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
         }
         if (lb > thi) break;  // every remaining candidate's t exceeds the best hit
         mask &= ~(1u << kb);
-        if (COUNT) count_exact(cnt);
+        if (COUNT) {
+            count_exact(cnt);
+            if (++n_exact == 2) cnt[CT_EXACT2]++;
+        }
         Real t;
         const bool hit = RT_NF_FUSED ? prim_exact_fused<Real>(S.prims[kb], ray_at_use<Real>(r), t)
                                      : prim_exact<Real>(S.prims[kb], ray_at_use<Real>(r), t);
