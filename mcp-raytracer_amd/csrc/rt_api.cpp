@@ -411,13 +411,13 @@ struct rt_camera {
         }
         // Stage-compacted pool kernel (pt_pool_kernel): possible for product brute-force
         // launches without an emission stack whose per-wave path pools fit in LDS beside
-        // the scene; the default in ref precision, where the diffuse stage it compacts is
-        // heaviest (Cornell 800^2 spp256: 19.15 vs 19.23 ms; fp32 15.48 vs 14.70 ms,
-        // profiles/r02/pool/). RT_AMD_POOL_KERNEL=0/1 overrides.
+        // the scene; the default in both precisions since its diffuse and trace queues are
+        // split by branch (Cornell 800^2 spp256 ref 16.82 ms vs chunked ~18.9 ms; fp32
+        // 14.12 vs 14.23 ms, profiles/r02/asplit/). RT_AMD_POOL_KERNEL=0/1 overrides.
         S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
         v.pool = !v.emit && count == 0 && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
                  (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
-                 env_flag("RT_AMD_POOL_KERNEL", prec == PREC_REF);
+                 env_flag("RT_AMD_POOL_KERNEL", true);
         int pass = 0;
         for (long t0 = 0; t0 < mine; t0 += pass_tiles, ++pass) {
             const long nt = std::min(pass_tiles, mine - t0);
