@@ -359,6 +359,15 @@ struct rt_camera {
         SampleBuf sb{};
         sb.rec = d_sbuf;
 
+        // Stage-compacted pool kernel (pt_pool_kernel): possible for product brute-force
+        // launches without an emission stack whose per-wave path pools fit in LDS beside
+        // the scene; the default in both precisions since its diffuse and trace queues are
+        // split by branch (Cornell 800^2 spp256 ref 16.82 ms vs chunked ~18.9 ms; fp32
+        // 14.12 vs 14.23 ms, profiles/r02/asplit/). RT_AMD_POOL_KERNEL=0/1 overrides.
+        S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
+        v.pool = !v.emit && count == 0 && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
+                 (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
+                 env_flag("RT_AMD_POOL_KERNEL", true);
         // guided schedule: half of the remaining samples per phase, chunks halving.
         // First-phase chunk from the samples per resident lane: an item is the
         // critical path of its pixel, so small per-launch workloads (a rank's
@@ -373,10 +382,18 @@ struct rt_camera {
             // launches (bounded per-ray cost: fewer atomics, Cornell 800^2 spp256 +2 %),
             // one otherwise (BVH scenes' heavy-tailed rays: wider takes cost spheres-500
             // 6-16 %; a rank's 1/2 share of Cornell: -9 %, 1/8: -4 %; profiles/r01/sweep_b/)
-            sb.pool = kWave * env_int("RT_AMD_POOL", v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
+            // The pool kernel (96 path slots per wave, any slot takes any item) wants wider takes
+            // and shorter first items: 4 tile-chunks per atomic from 256 samples per resident
+            // lane, 2 from 128, and first items of at most 8 samples (Cornell 800^2 spp256:
+            // N=1 16.84 -> 16.63 ms, a rank's 1/2 share 9.18 -> 8.43 ms; tools/sched_sweep.py,
+            // profiles/r02/sched/).
+            const int pool_auto = v.pool ? (spl >= 256.0 ? 4 : spl >= 128.0 ? 2 : 1)
+                                         : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
+            sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
             const double per = v.trav == TRAV_BRUTE ? 8.0 : 16.0;
+            const int c_max = v.pool ? 8 : 32;
             int c_auto = 1;
-            while (c_auto * 2 <= 32 && c_auto * 2 * per <= spl) c_auto *= 2;  // pow2 floor of spl / per, in [1, 32]
+            while (c_auto * 2 <= c_max && c_auto * 2 * per <= spl) c_auto *= 2;  // pow2 floor of spl / per, in [1, c_max]
             int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2)), np = 0;
             if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
                 c = std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples);
@@ -409,15 +426,6 @@ struct rt_camera {
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
         }
-        // Stage-compacted pool kernel (pt_pool_kernel): possible for product brute-force
-        // launches without an emission stack whose per-wave path pools fit in LDS beside
-        // the scene; the default in both precisions since its diffuse and trace queues are
-        // split by branch (Cornell 800^2 spp256 ref 16.82 ms vs chunked ~18.9 ms; fp32
-        // 14.12 vs 14.23 ms, profiles/r02/asplit/). RT_AMD_POOL_KERNEL=0/1 overrides.
-        S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
-        v.pool = !v.emit && count == 0 && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
-                 (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
-                 env_flag("RT_AMD_POOL_KERNEL", true);
         int pass = 0;
         for (long t0 = 0; t0 < mine; t0 += pass_tiles, ++pass) {
             const long nt = std::min(pass_tiles, mine - t0);
