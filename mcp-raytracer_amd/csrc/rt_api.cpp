@@ -332,14 +332,11 @@ struct rt_camera {
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
         S.lds_words = g.lds_level == 2 ? lds_words2 : lds_words;
-        // Fixed spp: the chunked kernel balances small images (few tiles per
-        // resident wave) far better; large images of LDS-resident scenes already
-        // balance over tiles and skip the sample-buffer round trip. Scenes
-        // traversed from global memory (long, variable per-sample cost: a tile
-        // waits for its slowest lane) take the chunked kernel at any size.
-        const long resident_waves = (long)cus * (kBlockChunk / kWave);
-        const bool big_scene = v.trav == TRAV_FAST && g.lds_level == 0;
-        const bool chunked = env_flag("RT_AMD_CHUNKED", mine < 4 * resident_waves || big_scene);
+        // Fixed spp: the chunked / pool kernels (per-sample records, in-order accumulate)
+        // at every size. Round 1 kept the sequential kernel for images of >= 4 tiles per
+        // resident wave; with the hand-out rules above the chunked kernel is faster there
+        // too (rain-50 1080p spp512: 50.7 -> 44.1 ms, profiles/r02/sched/), records and all.
+        const bool chunked = env_flag("RT_AMD_CHUNKED", true);
         if (C.adaptive || C.n_samples <= 0 || !chunked) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
             hip_check(hipEventRecord(pass_event(0, 0), stream), "hipEventRecord");
@@ -387,13 +384,22 @@ struct rt_camera {
             // lane, 2 from 128, and first items of at most 8 samples (Cornell 800^2 spp256:
             // N=1 16.84 -> 16.63 ms, a rank's 1/2 share 9.18 -> 8.43 ms; tools/sched_sweep.py,
             // profiles/r02/sched/).
+            // LDS-resident BVH scenes in the chunked kernel (resumable walks): 4 tile-chunks per
+            // atomic from 256 samples per resident lane (2 below) and a first chunk of the
+            // power-of-two floor of sqrt(spl) / 3 (spheres-500 800^2 spp64: N=1 6.62 -> 6.26 ms,
+            // rank shares N=2 3.54 -> 3.27, N=4 2.04 -> 1.78, N=8 1.21 -> 1.03 ms; rain-50 1080p
+            // spp512 rank shares N=2 31.5 -> 22.2 ms, N=8 7.8 -> 5.8 ms; profiles/r02/sched/).
+            // Trees walked from global memory keep 1 tile-chunk and spl / 16.
+            const bool bvh_lds = v.trav == TRAV_FAST && g.lds_level > 0;
             const int pool_auto = v.pool ? (spl >= 256.0 ? 4 : spl >= 128.0 ? 2 : 1)
-                                         : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
+                                 : bvh_lds ? (spl >= 256.0 ? 4 : 2)
+                                           : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
             const double per = v.trav == TRAV_BRUTE ? 8.0 : 16.0;
             const int c_max = v.pool ? 8 : 32;
+            const double c_target = bvh_lds ? std::sqrt(spl) / 3.0 : spl / per;
             int c_auto = 1;
-            while (c_auto * 2 <= c_max && c_auto * 2 * per <= spl) c_auto *= 2;  // pow2 floor of spl / per, in [1, c_max]
+            while (c_auto * 2 <= c_max && c_auto * 2 <= c_target) c_auto *= 2;  // pow2 floor, in [1, c_max]
             int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2)), np = 0;
             if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
                 c = std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples);
