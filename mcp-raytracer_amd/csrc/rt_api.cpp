@@ -389,15 +389,15 @@ struct rt_camera {
             // power-of-two floor of sqrt(spl) / 3 (spheres-500 800^2 spp64: N=1 6.62 -> 6.26 ms,
             // rank shares N=2 3.54 -> 3.27, N=4 2.04 -> 1.78, N=8 1.21 -> 1.03 ms; rain-50 1080p
             // spp512 rank shares N=2 31.5 -> 22.2 ms, N=8 7.8 -> 5.8 ms; profiles/r02/sched/).
-            // Trees walked from global memory keep 1 tile-chunk and spl / 16.
-            const bool bvh_lds = v.trav == TRAV_FAST && g.lds_level > 0;
+            // Trees walked from global memory (a sample costs ~150 us of a lane at config 5) cap
+            // the first chunk at 4 (config 5, 4096^2 spp1024: 9617 -> 8980 ms per frame).
+            const bool bvh = v.trav == TRAV_FAST;
             const int pool_auto = v.pool ? (spl >= 256.0 ? 4 : spl >= 128.0 ? 2 : 1)
-                                 : bvh_lds ? (spl >= 256.0 ? 4 : 2)
-                                           : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
+                                 : bvh ? (spl >= 256.0 ? 4 : 2)
+                                       : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
-            const double per = v.trav == TRAV_BRUTE ? 8.0 : 16.0;
-            const int c_max = v.pool ? 8 : 32;
-            const double c_target = bvh_lds ? std::sqrt(spl) / 3.0 : spl / per;
+            const int c_max = v.pool ? 8 : (bvh && g.lds_level == 0) ? 4 : 32;
+            const double c_target = bvh ? std::sqrt(spl) / 3.0 : spl / 8.0;
             int c_auto = 1;
             while (c_auto * 2 <= c_max && c_auto * 2 <= c_target) c_auto *= 2;  // pow2 floor, in [1, c_max]
             int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2)), np = 0;

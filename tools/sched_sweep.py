@@ -21,7 +21,8 @@ def main():
     scene = sys.argv[1] if len(sys.argv) > 1 else "cornell"
     extra = {"cornell": {"width": 800, "samples": 256, "depth": 16},
              "spheres": {"width": 800, "samples": 64, "depth": 8},
-             "rain": {"width": 1920, "samples": 512, "depth": 16}}[scene]
+             "rain": {"width": 1920, "samples": 512, "depth": 16},
+             "spheres100k": {"width": int(os.environ.get("SWEEP_W", "2048")), "samples": 64, "depth": 100}}[scene]
     cfg, ex, _ = SCENES[scene]
     cam = rt.create_camera_from_scene_data(rt.generate_scene_data(cfg), {**extra, **ex, "aTolerance": 0})
     frame = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.uint8, device="cuda")
