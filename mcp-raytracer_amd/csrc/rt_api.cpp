@@ -372,13 +372,10 @@ struct rt_camera {
         // grazing a field of spheres) need short items, while large ones amortise
         // the hand-out over long items (tools/tail_probe.py sweep).
         {
-            // BVH scenes have heavy-tailed per-ray cost (grazing rays): spl / 16; brute-force
-            // scenes test every primitive per ray (bounded cost): spl / 8
+            // spl: samples per resident lane of this launch.
             const double spl = (double)mine * kWave * (double)C.n_samples / ((double)cus * kBlockChunk);
-            // items a wave takes per global atomic: two tile-chunks for large brute-force
-            // launches (bounded per-ray cost: fewer atomics, Cornell 800^2 spp256 +2 %),
-            // one otherwise (BVH scenes' heavy-tailed rays: wider takes cost spheres-500
-            // 6-16 %; a rank's 1/2 share of Cornell: -9 %, 1/8: -4 %; profiles/r01/sweep_b/)
+            // Brute-force scenes in the chunked kernel: two tile-chunks per atomic from 512 spl
+            // and first items of spl / 8 (round 1, profiles/r01/sweep_b/).
             // The pool kernel (96 path slots per wave, any slot takes any item) wants wider takes
             // and shorter first items: 4 tile-chunks per atomic from 256 samples per resident
             // lane, 2 from 128, and first items of at most 8 samples (Cornell 800^2 spp256:
