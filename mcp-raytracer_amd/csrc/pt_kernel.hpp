@@ -1731,16 +1731,23 @@ __device__ __forceinline__ int shade_hit(const DevScene& S, Path<EMIT>& P, int h
 // 0.5/nL...]) generate + value and the throughput update (camera.ts:263-315).
 // Returns true when the path ends here (mixture value <= 0.0001: the caller's
 // sample radiance is the level's emission); else P continues from p.
-template <class Real, bool EMIT, bool COUNT, bool PROF>
+// BR: 0 = the mixture's branch decided here; 1 / 2 = the caller knows it is the
+// cosine / light branch (pool kernel: the draw was classified ahead) - the light
+// branch then needs only the ONB's w (CosinePDF.value), not u and v.
+template <class Real, bool EMIT, bool COUNT, bool PROF, int BR = 0>
 __device__ __forceinline__ bool shade_diffuse(const DevScene& S, const RtCamera& C, Path<EMIT>& P, int h, bool planar,
                                               bool front, V3 p, V3 nrm, V3 att, uint32_t* cnt, Prof& pf) {
     if (COUNT) cnt[CT_DIFFUSE]++;
     Onb b;
     if (planar && h < S.n_onb) {
         const RtOnb& ob = S.onbs[(h * 2 + (sizeof(Real) == 4 ? 1 : 0)) * 2 + (front ? 0 : 1)];
-        b.u = ld3(ob.u);
-        b.v = ld3(ob.v);
+        if (BR != 2) {
+            b.u = ld3(ob.u);
+            b.v = ld3(ob.v);
+        }
         b.w = ld3(ob.w);
+    } else if (BR == 2) {
+        b.w = unit<Real>(nrm);  // make_onb's w
     } else {
         b = make_onb<Real>(nrm);
     }
@@ -1751,7 +1758,7 @@ __device__ __forceinline__ bool shade_diffuse(const DevScene& S, const RtCamera&
     const Real rnd = total1 ? u0 : u0 * total;
     Real partial = (Real)0.5;
     V3 gdir;
-    if (rnd < partial || C.n_lights == 0) {
+    if (BR == 1 || (BR == 0 && (rnd < partial || C.n_lights == 0))) {
         const Real r1 = uniform<Real>(P.rng);
         const Real r2 = uniform<Real>(P.rng);
         const Real phi = (Real)2 * K<Real>::PI * r1;
@@ -2466,8 +2473,14 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 int s = __float_as_int(g2.w);
                 phase = P.bounces;
                 const RtCamera& C = cam_opaque();
-                if (shade_diffuse<Real, false, false, false>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
-                                                             V3{g4.x, g4.y, g4.z}, cnt, pf)) {
+                const bool dterm =
+                    !RT_POOL_DSPLIT ? shade_diffuse<Real, false, false, false, 0>(S, C, P, h, (hf >> 30) & 1, hf < 0,
+                                                                                  P.o, P.d, V3{g4.x, g4.y, g4.z}, cnt, pf)
+                    : dtop ? shade_diffuse<Real, false, false, false, 2>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
+                                                                         V3{g4.x, g4.y, g4.z}, cnt, pf)
+                           : shade_diffuse<Real, false, false, false, 1>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
+                                                                         V3{g4.x, g4.y, g4.z}, cnt, pf);
+                if (dterm) {
                     // mixture value cut-off: the level's emission (as computed at the hit: T is unchanged)
                     const V3 c = mulv(ld3(S.mats[S.prims[h].mat].emitted), P.T);
                     phase = record(c, P.bounces, slot, s, s_end);
