@@ -1242,9 +1242,38 @@ __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Rea
     return true;
 }
 
-template <class Real, bool COUNT>
+// The brute-force pass's version over an RtPre record {n[a], D, Q[ia], Q[ib], w_a*v, w_a*u,
+// max(|Q[ia]|, |Q[ib]|)}: the hit-point error of both in-plane coordinates bounded by one
+// per-ray term (|o| <= on, |d| <= dn, |Q| <= qm), alpha and beta through the host-folded
+// products - fewer operations, a (slightly) wider but still conservative margin.
+template <int CODE>
+__device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, float& lo) {
+    constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
+    constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+    const float na = v[0], D = v[1], q1 = v[2], q2 = v[3], asv = v[4], asu = v[5], qm = v[6];
+    const float denom = na * f.d[a];
+    lo = kTminLo;
+    if (!(::fabsf(denom) > 1e-3f * f.dn)) return true;  // near-parallel: decide exactly
+    const float no = na * f.o[a];
+    const float idn = __builtin_amdgcn_rcpf(denom);
+    const float t = (D - no) * idn;
+    const float et = kRel * ((::fabsf(D) + ::fabsf(no)) * ::fabsf(idn) + 2.0f * ::fabsf(t)) + 1e-30f;
+    if (t + et < kTminLo) return false;
+    lo = t - et;
+    const float alpha = (f.o[ia] + t * f.d[ia] - q1) * asv;
+    const float beta = (f.o[ib] + t * f.d[ib] - q2) * asu;
+    const float dp = et * f.dn + kRel * (f.on + ::fabsf(t) * f.dn + qm);
+    const float ea = ::fabsf(asv) * dp + 1e-4f, eb = ::fabsf(asu) * dp + 1e-4f;
+    return !(alpha < -ea || alpha > 1.0f + ea || beta < -eb || beta > 1.0f + eb);
+}
+
+struct NoHook {
+    __device__ void operator()() const {}
+};
+// `after_prefilter`: called once the pre-filter pass is done (diagnostic section timer).
+template <class Real, bool COUNT, class Hook = NoHook>
 __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
-                                                    float* lot, uint32_t* cnt) {
+                                                    float* lot, uint32_t* cnt, Hook after_prefilter = Hook()) {
     const FRay f = make_fray(r.o, r.d);
     uint32_t mask = 0u;
     for (int k = 0; k < n_prims; ++k) {
@@ -1257,14 +1286,13 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
         } else if (q.kind != PRE_OTHER) {
             if (COUNT) cnt[CT_QUAD]++;
             const float* v = q.f;
-            const float inf = __builtin_inff();
             switch (q.kind) {
-                case 1: maybe = aquad_maybe_v<1>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
-                case 2: maybe = aquad_maybe_v<2>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
-                case 3: maybe = aquad_maybe_v<3>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
-                case 4: maybe = aquad_maybe_v<4>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
-                case 5: maybe = aquad_maybe_v<5>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
-                default: maybe = aquad_maybe_v<6>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], f.o, f.d, f.dn, inf, lo); break;
+                case 1: maybe = aquad_maybe_pre<1>(v, f, lo); break;
+                case 2: maybe = aquad_maybe_pre<2>(v, f, lo); break;
+                case 3: maybe = aquad_maybe_pre<3>(v, f, lo); break;
+                case 4: maybe = aquad_maybe_pre<4>(v, f, lo); break;
+                case 5: maybe = aquad_maybe_pre<5>(v, f, lo); break;
+                default: maybe = aquad_maybe_pre<6>(v, f, lo); break;
             }
         } else {
             maybe = prim_maybe<COUNT>(ld_uniform(S.gprims, k), f, lo, cnt);
@@ -1274,6 +1302,7 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
             mask |= 1u << k;
         }
     }
+    after_prefilter();
     Real best_t = (Real)__builtin_inf();
     int best = -1;
     float thi = __builtin_inff();
@@ -2348,6 +2377,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 #ifndef RT_POOL_DSPLIT
 #define RT_POOL_DSPLIT 1
 #endif
+#ifndef RT_POOL_PROF
+#define RT_POOL_PROF 0  // diagnostic variant: section timing (INSTR == 2 launches) in the pool kernel
+#endif
 #ifndef RT_POOL_ASPLIT
 #define RT_POOL_ASPLIT 1  // A queue split: paths to start (and slots needing an item) | paths in flight
 #endif
@@ -2410,7 +2442,10 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     const double rtx = 1.0 / (double)tiles_x;
     uint32_t* cnt = nullptr;  // product build: no work counters
     unsigned long long st_err = 0;
+    constexpr bool PP = RT_POOL_PROF;
+    __shared__ unsigned long long prof_lds[PP ? kProfWaves * kProfSlot : 1];
     Prof pf;
+    prof_init<PP>(pf, prof_lds, lane);
 
     for (int k = lane; k < kPoolK; k += kWave) {
         qa[k] = (uint8_t)k;
@@ -2440,6 +2475,8 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     while (a_cnt + d_cnt + dl_cnt > 0) {
         // other lanes' slot and queue writes of the previous trip (one wave: LDS is in order)
         __asm__ volatile("" ::: "memory");
+        prof_trip<PP>(pf);
+        psec<PP>(pf, PR_ACC);  // the previous trip's records, slot stores and queue appends
         const bool dtop = RT_POOL_DSPLIT && dl_cnt > d_cnt;  // the longer D stack
         const int dn = dtop ? dl_cnt : d_cnt;
         const bool atop = RT_POOL_ASPLIT && ac_cnt > an_cnt;  // the longer A stack
@@ -2474,12 +2511,12 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 phase = P.bounces;
                 const RtCamera& C = cam_opaque();
                 const bool dterm =
-                    !RT_POOL_DSPLIT ? shade_diffuse<Real, false, false, false, 0>(S, C, P, h, (hf >> 30) & 1, hf < 0,
-                                                                                  P.o, P.d, V3{g4.x, g4.y, g4.z}, cnt, pf)
-                    : dtop ? shade_diffuse<Real, false, false, false, 2>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
-                                                                         V3{g4.x, g4.y, g4.z}, cnt, pf)
-                           : shade_diffuse<Real, false, false, false, 1>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
-                                                                         V3{g4.x, g4.y, g4.z}, cnt, pf);
+                    !RT_POOL_DSPLIT ? shade_diffuse<Real, false, false, PP, 0>(S, C, P, h, (hf >> 30) & 1, hf < 0,
+                                                                               P.o, P.d, V3{g4.x, g4.y, g4.z}, cnt, pf)
+                    : dtop ? shade_diffuse<Real, false, false, PP, 2>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
+                                                                      V3{g4.x, g4.y, g4.z}, cnt, pf)
+                           : shade_diffuse<Real, false, false, PP, 1>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
+                                                                      V3{g4.x, g4.y, g4.z}, cnt, pf);
                 if (dterm) {
                     // mixture value cut-off: the level's emission (as computed at the hit: T is unchanged)
                     const V3 c = mulv(ld3(S.mats[S.prims[h].mat].emitted), P.T);
@@ -2570,20 +2607,27 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                     P.em_n = 0;
                 }
                 V3 c;
-                bool term = path_pre<Real, false, false>(C, P, pf, c);
+                psec<PP>(pf, PR_NEWPATH);  // item hand-out and path starts
+                bool term = path_pre<Real, false, PP>(C, P, pf, c);
                 V3 att;
                 int hf = 0;
                 if (!term) {
                     const RayK<Real> ray = make_ray<Real>(P.o, P.d);
                     Real t;
-                    const int h = closest_hit_any<Real, false, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
+                    int h;
+                    if (PP && TRAV == TRAV_BRUTE && RT_BRUTE_DEFER && C.n_prims <= kBruteMaxPrims)  // section timer
+                        h = closest_hit_brute_nf<Real, false>(S, C.n_prims, ray, t, reinterpret_cast<float*>(stk), cnt,
+                                                              [&]() { psec<PP>(pf, PR_TILE); });
+                    else
+                        h = closest_hit_any<Real, false, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
+                    psec<PP>(pf, PR_HIT);
                     if (h < 0) {
                         term = true;
-                        c = miss_color<Real, false, false>(C, P, st_err, pf);
+                        c = miss_color<Real, false, PP>(C, P, st_err, pf);
                     } else {
                         V3 p, nrm, emitted, sdir;
                         bool front, planar;
-                        const int kind = shade_hit<Real, false, false, false>(S, P, h, t, cnt, pf, p, nrm, front,
+                        const int kind = shade_hit<Real, false, false, PP>(S, P, h, t, cnt, pf, p, nrm, front,
                                                                               planar, emitted, att, sdir);
                         if (kind == SC_NONE) {
                             term = true;
@@ -2639,6 +2683,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     }
     PixStats st;
     publish_stats(out, st, st_err, lane);
+    publish_counters<false, PP>(out, cnt, pf, lane);
 }
 
 }  // namespace rt

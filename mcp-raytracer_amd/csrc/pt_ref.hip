@@ -9,7 +9,7 @@ template <bool EMIT, int INSTR, int TRAV, int LDSS>
 static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                       const SampleBuf* sb, bool pool, hipStream_t stream) {
     if (sb && pool) {  // stage-compacted pool kernel: product brute-force builds only
-        if constexpr (!EMIT && INSTR == 0 && TRAV == TRAV_BRUTE) {
+        if constexpr (!EMIT && (INSTR == 0 || (RT_POOL_PROF && INSTR == 2)) && TRAV == TRAV_BRUTE) {
             hipLaunchKernelGGL((pt_pool_kernel<double, TRAV, LDSS>), dim3(g.grid), dim3(kBlockPool), g.lds_bytes, stream,
                                S, reg, out, g.tiles_x, *sb);
             return hipGetLastError();

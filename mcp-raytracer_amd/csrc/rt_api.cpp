@@ -174,9 +174,9 @@ struct rt_camera {
                 q.f[1] = p.g0[3];
                 q.f[2] = p.g0[ia];
                 q.f[3] = p.g0[ib];
-                q.f[4] = p.g3[3];
-                q.f[5] = p.g2[3];
-                q.f[6] = p.g1[3];
+                q.f[4] = p.g3[3] * p.g2[3];  // w_a * v (alpha's factor)
+                q.f[5] = p.g3[3] * p.g1[3];  // w_a * u (beta's factor)
+                q.f[6] = std::max(std::fabs(p.g0[ia]), std::fabs(p.g0[ib]));
             } else {
                 q.kind = PRE_OTHER;
             }
@@ -362,7 +362,7 @@ struct rt_camera {
         // split by branch (Cornell 800^2 spp256 ref 16.82 ms vs chunked ~18.9 ms; fp32
         // 14.12 vs 14.23 ms, profiles/r02/asplit/). RT_AMD_POOL_KERNEL=0/1 overrides.
         S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
-        v.pool = !v.emit && count == 0 && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
+        v.pool = !v.emit && (count == 0 || (RT_POOL_PROF && count == 2 && prec == PREC_REF)) && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
                  (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
         // guided schedule: half of the remaining samples per phase, chunks halving.

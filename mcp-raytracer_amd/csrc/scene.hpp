@@ -99,7 +99,8 @@ static_assert(sizeof(RtMat) == 64, "RtMat must be 64 bytes");
 // fp32 pre-filter of a sphere or an axis-aligned quad reads, in one 32-byte scalar
 // load (the full RtPrim takes two dependent loads for a quad: its type, then its
 // axis code). kind: PRE_SPHERE {cx, cy, cz, r}; 1..6 = axis code {n[a], D, Q[ia],
-// Q[ib], +-w[a], v[iv], u[iu]} (scene.cpp encode_axis_quad); PRE_OTHER: read the RtPrim.
+// Q[ib], +-w[a]*v[iv], +-w[a]*u[iu], max(|Q[ia]|, |Q[ib]|)} (scene.cpp encode_axis_quad);
+// PRE_OTHER: read the RtPrim.
 enum : int32_t { PRE_SPHERE = 0, PRE_OTHER = 7 };
 struct alignas(16) RtPre {
     int32_t kind;
