@@ -1402,12 +1402,13 @@ enum ScatterKind { SC_NONE = 0, SC_SPEC = 1, SC_PDF = 2 };
 // their children iteratively (mixedMaterial.ts:38-44, layeredMaterial.ts:36-53).
 template <class Real>
 __device__ __forceinline__ int scatter(const DevScene& S, int mi, V3 din, V3 n, bool front, uint64_t& rng, V3& att,
-                                       V3& dir) {
+                                       V3& dir, int* pdf_mat = nullptr) {
     while (true) {
         const RtMat m = S.mats[mi];
         switch (m.type) {
             case MAT_LAMBERT:
                 att = ld3(m.color);
+                if (pdf_mat) *pdf_mat = mi;  // att is this material's albedo
                 return SC_PDF;
             case MAT_METAL: {
                 const V3 refl = reflect<Real>(unit<Real>(din), n);
@@ -1734,7 +1735,8 @@ __device__ __forceinline__ V3 miss_color(const RtCamera& C, const Path<EMIT>& P,
 // `planar` = the primitive has a fixed normal (quad / plane: ONB table lookup).
 template <class Real, bool EMIT, bool COUNT, bool PROF>
 __device__ __forceinline__ int shade_hit(const DevScene& S, Path<EMIT>& P, int h, Real t, uint32_t* cnt, Prof& pf,
-                                         V3& p, V3& nrm, bool& front, bool& planar, V3& emitted, V3& att, V3& sdir) {
+                                         V3& p, V3& nrm, bool& front, bool& planar, V3& emitted, V3& att, V3& sdir,
+                                         int* pdf_mat = nullptr) {
     if (COUNT) cnt[CT_MATERIAL]++;
     const RtPrim pr = S.prims[h];
     p = ray_at<Real>(P.o, P.d, t);
@@ -1751,7 +1753,7 @@ __device__ __forceinline__ int shade_hit(const DevScene& S, Path<EMIT>& P, int h
     const RtMat hm = S.mats[pr.mat];
     emitted = mulv(ld3(hm.emitted), P.T);
     psec<PROF>(pf, PR_HITREC);
-    const int kind = scatter<Real>(S, pr.mat, P.d, nrm, front, P.rng, att, sdir);
+    const int kind = scatter<Real>(S, pr.mat, P.d, nrm, front, P.rng, att, sdir, pdf_mat);
     psec<PROF>(pf, PR_SCATTER);
     return kind;
 }
@@ -2369,7 +2371,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 // bit-identical.
 // ---------------------------------------------------------------------------
 #ifndef RT_POOL_K
-#define RT_POOL_K 96
+#define RT_POOL_K 119  // 64-byte slots + 2 queue bytes: 119 per wave fill the 7.8 KB an 80-byte slot's 96 took
 #endif
 #ifndef RT_POOL_BLOCK
 #define RT_POOL_BLOCK 1024
@@ -2385,17 +2387,32 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 #endif
 constexpr int kPoolK = RT_POOL_K;          // path slots per wave
 constexpr int kBlockPool = RT_POOL_BLOCK;  // persistent workgroup size
-constexpr int kPoolGroups = 5;             // 16-byte groups per slot (below)
+constexpr int kPoolGroups = 4;             // 16-byte groups per slot (below)
 static_assert(kPoolK >= kWave && kPoolK <= 256, "pool slots: one full wave, u8 queue entries");
 // Per wave: slot state as [group][slot] float4, then the A queue (a ring) and the D queue
 // (u8 slot indices; with RT_POOL_DSPLIT two stacks in one array: cosine-branch paths from
 // the bottom, light-branch paths from the top - together at most kPoolK entries).
-//   g0 {rng lo, rng hi, phase, s_end}  phase: bounces so far (>= 0), PH_NEW or PH_ITEM
+// 64 bytes per slot (more slots per wave fill more trips: 64 / 80 / 96 slots ran Cornell in
+// 21.7 / 17.7 / 16.1 ms, profiles/r02/poolsize/):
+//   g0 {rng lo, rng hi, meta, hf}   meta = (phase + 2) | lambert material << 8 (D only),
+//                                   phase: bounces so far (>= 0), PH_NEW or PH_ITEM;
+//                                   hf = h | planar << 30 | front << 31 (D only)
 //   g1 {o (hit point p when queued for D), slot}
-//   g2 {d (the face normal when queued for D), s}
+//   g2 {d (the face normal when queued for D), s | s_end << 16}
 //   g3 {T, i | j << 16}
-//   g4 {attenuation, h | planar << 30 | front << 31}   (D only)
+// The D stage reads the Lambertian albedo (the scatter's attenuation) from the material
+// table. Host gates: spp <= 65535, depth <= 250, materials < 2^24.
 constexpr size_t kPoolWaveBytes = ((size_t)kPoolK * kPoolGroups * 16 + 2 * kPoolK + 15) / 16 * 16;
+__device__ __forceinline__ float pool_meta(int phase, int mat) {
+    return __uint_as_float((uint32_t)((phase + 2) & 0xff) | ((uint32_t)mat << 8));
+}
+__device__ __forceinline__ int meta_phase(float m) { return (int)(__float_as_uint(m) & 0xffu) - 2; }
+__device__ __forceinline__ int meta_mat(float m) { return (int)(__float_as_uint(m) >> 8); }
+__device__ __forceinline__ float pool_ss(int s, int s_end) {
+    return __uint_as_float((uint32_t)s | ((uint32_t)s_end << 16));
+}
+__device__ __forceinline__ int ss_s(float v) { return (int)(__float_as_uint(v) & 0xffffu); }
+__device__ __forceinline__ int ss_end(float v) { return (int)(__float_as_uint(v) >> 16); }
 constexpr size_t pool_lds_bytes() { return (size_t)(kBlockPool / kWave) * kPoolWaveBytes; }
 enum : int { PH_NEW = -1, PH_ITEM = -2 };  // next sample's path to start / no work item
 
@@ -2449,7 +2466,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
 
     for (int k = lane; k < kPoolK; k += kWave) {
         qa[k] = (uint8_t)k;
-        G[k] = make_float4(0.f, 0.f, __int_as_float(PH_ITEM), 0.f);
+        G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0), 0.f);
     }
     int a_head = 0, a_cnt = kPoolK, d_head = 0, d_cnt = 0;  // wave-uniform queue state
     int dl_cnt = 0;  // RT_POOL_DSPLIT: light-branch stack (d_cnt: cosine-branch stack)
@@ -2495,37 +2512,36 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 d_cnt -= n;
             }
             if (k >= 0) {
-                const float4 g0 = G[k], g1 = G[kPoolK + k], g2 = G[2 * kPoolK + k], g3 = G[3 * kPoolK + k],
-                             g4 = G[4 * kPoolK + k];
+                const float4 g0 = G[k], g1 = G[kPoolK + k], g2 = G[2 * kPoolK + k], g3 = G[3 * kPoolK + k];
                 Path<false> P;
                 P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
-                P.bounces = __float_as_int(g0.z);
+                P.bounces = meta_phase(g0.z);
                 P.em_n = 0;
                 P.o = V3{g1.x, g1.y, g1.z};
                 P.d = V3{g2.x, g2.y, g2.z};
                 P.T = V3{g3.x, g3.y, g3.z};
-                const int hf = __float_as_int(g4.w);
+                const int hf = __float_as_int(g0.w);
                 const int h = hf & 0x3fffffff;
-                const int s_end = __float_as_int(g0.w), slot = __float_as_int(g1.w);
-                int s = __float_as_int(g2.w);
+                const V3 att = ld3(S.mats[meta_mat(g0.z)].color);  // the Lambertian scatter's attenuation
+                const int s_end = ss_end(g2.w), slot = __float_as_int(g1.w);
+                int s = ss_s(g2.w);
                 phase = P.bounces;
                 const RtCamera& C = cam_opaque();
                 const bool dterm =
                     !RT_POOL_DSPLIT ? shade_diffuse<Real, false, false, PP, 0>(S, C, P, h, (hf >> 30) & 1, hf < 0,
-                                                                               P.o, P.d, V3{g4.x, g4.y, g4.z}, cnt, pf)
+                                                                               P.o, P.d, att, cnt, pf)
                     : dtop ? shade_diffuse<Real, false, false, PP, 2>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
-                                                                      V3{g4.x, g4.y, g4.z}, cnt, pf)
+                                                                      att, cnt, pf)
                            : shade_diffuse<Real, false, false, PP, 1>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
-                                                                      V3{g4.x, g4.y, g4.z}, cnt, pf);
+                                                                      att, cnt, pf);
                 if (dterm) {
                     // mixture value cut-off: the level's emission (as computed at the hit: T is unchanged)
                     const V3 c = mulv(ld3(S.mats[S.prims[h].mat].emitted), P.T);
                     phase = record(c, P.bounces, slot, s, s_end);
                 }
                 G[k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
-                                   __int_as_float(phase), g0.w);
-                G[kPoolK + k] = make_float4(P.o.x, P.o.y, P.o.z, g1.w);
-                G[2 * kPoolK + k] = make_float4(P.d.x, P.d.y, P.d.z, __int_as_float(s));
+                                   pool_meta(phase, 0), 0.f);
+                G[2 * kPoolK + k] = make_float4(P.d.x, P.d.y, P.d.z, pool_ss(s, s_end));
                 G[3 * kPoolK + k] = make_float4(P.T.x, P.T.y, P.T.z, g3.w);
             }
             if (RT_POOL_ASPLIT) {
@@ -2549,15 +2565,15 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 a_head = pool_ring(a_head + n);
                 a_cnt -= n;
             }
-            float4 g0 = make_float4(0.f, 0.f, __int_as_float(PH_ITEM), 0.f), g1 = g0, g2 = g0, g3 = g0;
+            float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0), 0.f), g1 = g0, g2 = g0, g3 = g0;
             if (k >= 0) {
                 g0 = G[k];
                 g1 = G[kPoolK + k];
                 g2 = G[2 * kPoolK + k];
                 g3 = G[3 * kPoolK + k];
             }
-            int phase = __float_as_int(g0.z), s_end = __float_as_int(g0.w), slot = __float_as_int(g1.w);
-            int s = __float_as_int(g2.w), ij = __float_as_int(g3.w);
+            int phase = meta_phase(g0.z), s_end = ss_end(g2.w), slot = __float_as_int(g1.w);
+            int s = ss_s(g2.w), ij = __float_as_int(g3.w);
             // work items for slots without one (the chunked kernel's guided hand-out)
             const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
             if (need != 0ull && !exhausted) {
@@ -2610,7 +2626,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 psec<PP>(pf, PR_NEWPATH);  // item hand-out and path starts
                 bool term = path_pre<Real, false, PP>(C, P, pf, c);
                 V3 att;
-                int hf = 0;
+                int hf = 0, dmat = 0;
                 if (!term) {
                     const RayK<Real> ray = make_ray<Real>(P.o, P.d);
                     Real t;
@@ -2628,7 +2644,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                         V3 p, nrm, emitted, sdir;
                         bool front, planar;
                         const int kind = shade_hit<Real, false, false, PP>(S, P, h, t, cnt, pf, p, nrm, front,
-                                                                              planar, emitted, att, sdir);
+                                                                              planar, emitted, att, sdir, &dmat);
                         if (kind == SC_NONE) {
                             term = true;
                             c = emitted;
@@ -2654,11 +2670,12 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 }
                 phase = term ? record(c, P.bounces, slot, s, s_end) : P.bounces;
                 g0 = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
-                                 __int_as_float(phase), __int_as_float(s_end));
+                                 pool_meta(phase, to_d ? dmat : 0), __int_as_float(hf));
                 g1 = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
-                g2 = make_float4(P.d.x, P.d.y, P.d.z, __int_as_float(s));
+                g2 = make_float4(P.d.x, P.d.y, P.d.z, pool_ss(s, s_end));
                 g3 = make_float4(P.T.x, P.T.y, P.T.z, __int_as_float(ij));
-                if (to_d) G[4 * kPoolK + k] = make_float4(att.x, att.y, att.z, __int_as_float(hf));
+            } else if (keep) {  // a slot still waiting for a work item
+                g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0), 0.f);
             }
             if (keep) {
                 G[k] = g0;

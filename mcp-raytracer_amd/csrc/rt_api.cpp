@@ -363,6 +363,7 @@ struct rt_camera {
         // 14.12 vs 14.23 ms, profiles/r02/asplit/). RT_AMD_POOL_KERNEL=0/1 overrides.
         S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
         v.pool = !v.emit && (count == 0 || (RT_POOL_PROF && count == 2 && prec == PREC_REF)) && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
+                 C.n_samples <= 65535 && C.depth <= 250 && build.mats.size() < (1u << 24) &&  // 64-byte slot fields
                  (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
         // guided schedule: half of the remaining samples per phase, chunks halving.
