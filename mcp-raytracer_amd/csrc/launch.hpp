@@ -60,7 +60,7 @@ hipError_t launch_tiles_unpack(const void* slabs, int groups, int slab_tiles, co
 // per-lane candidate bounds of the nearest-first brute force.
 inline size_t stack_lds_bytes(int stack_depth, int trav, int n_prims) {
     if (trav == TRAV_BRUTE)  // larger forced brute-force scenes take the in-order loop (no LDS)
-        return RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims ? (size_t)std::max(n_prims, 1) * kStackStride * sizeof(float)
+        return RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims ? (size_t)std::max(n_prims, 1) * kStackStride * sizeof(uint16_t)
                                                            : 0;
     const size_t d = (size_t)(stack_depth > 0 ? stack_depth : 1);
     return d * kStackStride * ((trav == TRAV_FAST && kStackTnear) ? 2 * sizeof(int) : sizeof(int));

@@ -1267,13 +1267,29 @@ __device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, f
     return !(alpha < -ea || alpha > 1.0f + ea || beta < -eb || beta > 1.0f + eb);
 }
 
+// The brute-force pass's per-lane candidate bounds live in fp16 LDS columns (half the
+// LDS of fp32: room for more pool slots). A stored bound must stay a lower bound: clamped
+// at 0 (every hit has t > 0.001) and converted toward zero (v_cvt_pkrtz: round down for
+// non-negative values; above 65504 it saturates to 65504, still below); NaN stays NaN
+// (such a candidate is always tested).
+__device__ __forceinline__ uint16_t lot_store(float lo) {
+    const float v = lo != lo ? lo : ::fmaxf(lo, 0.0f);
+    const auto h = __builtin_amdgcn_cvt_pkrtz(v, 0.0f);
+    return __builtin_bit_cast(uint16_t, h[0]);
+}
+__device__ __forceinline__ float lot_load(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
+// This lane's fp16 column base (stk = the block's LDS base + threadIdx.x, as int*).
+__device__ __forceinline__ uint16_t* lot_column(int* stk) {
+    return reinterpret_cast<uint16_t*>(stk - threadIdx.x) + threadIdx.x;
+}
+
 struct NoHook {
     __device__ void operator()() const {}
 };
 // `after_prefilter`: called once the pre-filter pass is done (diagnostic section timer).
 template <class Real, bool COUNT, class Hook = NoHook>
 __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
-                                                    float* lot, uint32_t* cnt, Hook after_prefilter = Hook()) {
+                                                    uint16_t* lot, uint32_t* cnt, Hook after_prefilter = Hook()) {
     const FRay f = make_fray(r.o, r.d);
     uint32_t mask = 0u;
     for (int k = 0; k < n_prims; ++k) {
@@ -1298,7 +1314,7 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
             maybe = prim_maybe<COUNT>(ld_uniform(S.gprims, k), f, lo, cnt);
         }
         if (maybe) {
-            lot[k * kStackStride] = lo;
+            lot[k * kStackStride] = lot_store(lo);
             mask |= 1u << k;
         }
     }
@@ -1314,10 +1330,10 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
     while (mask != 0u) {
         // nearest remaining candidate (a NaN bound is never skipped: it is tested exactly)
         int kb = __builtin_ctz(mask);
-        float lb = lot[kb * kStackStride];
+        float lb = lot_load(lot[kb * kStackStride]);
         for (uint32_t m = mask & (mask - 1u); m != 0u; m &= m - 1u) {
             const int k = __builtin_ctz(m);
-            const float l = lot[k * kStackStride];
+            const float l = lot_load(lot[k * kStackStride]);
             if (l < lb) {
                 lb = l;
                 kb = k;
@@ -1576,7 +1592,7 @@ __device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, c
                                                float* stkt, uint32_t* cnt) {
     if (TRAV == TRAV_BRUTE) {
         if (RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims)
-            return closest_hit_brute_nf<Real, COUNT>(S, n_prims, r, t, reinterpret_cast<float*>(stk), cnt);
+            return closest_hit_brute_nf<Real, COUNT>(S, n_prims, r, t, lot_column(stk), cnt);
         return closest_hit_brute<Real, COUNT>(S, n_prims, r, t, cnt);
     }
     if (trav_fast(TRAV)) return closest_hit_fast<Real, COUNT, TRAV == TRAV_FAST_DEFER>(S, r, t, stk, stkt, cnt);
@@ -2371,7 +2387,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 // bit-identical.
 // ---------------------------------------------------------------------------
 #ifndef RT_POOL_K
-#define RT_POOL_K 119  // 64-byte slots + 2 queue bytes: 119 per wave fill the 7.8 KB an 80-byte slot's 96 took
+#define RT_POOL_K 134  // 64-byte slots + 2 queue bytes per wave, beside fp16 candidate columns
 #endif
 #ifndef RT_POOL_BLOCK
 #define RT_POOL_BLOCK 1024
@@ -2632,7 +2648,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                     Real t;
                     int h;
                     if (PP && TRAV == TRAV_BRUTE && RT_BRUTE_DEFER && C.n_prims <= kBruteMaxPrims)  // section timer
-                        h = closest_hit_brute_nf<Real, false>(S, C.n_prims, ray, t, reinterpret_cast<float*>(stk), cnt,
+                        h = closest_hit_brute_nf<Real, false>(S, C.n_prims, ray, t, lot_column(stk), cnt,
                                                               [&]() { psec<PP>(pf, PR_TILE); });
                     else
                         h = closest_hit_any<Real, false, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
