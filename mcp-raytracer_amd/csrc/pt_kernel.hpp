@@ -2387,7 +2387,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 // bit-identical.
 // ---------------------------------------------------------------------------
 #ifndef RT_POOL_K
-#define RT_POOL_K 134  // 64-byte slots + 2 queue bytes per wave, beside fp16 candidate columns
+#define RT_POOL_K 152  // 56-byte slots + 2 queue bytes per wave, beside fp16 candidate columns
 #endif
 #ifndef RT_POOL_BLOCK
 #define RT_POOL_BLOCK 1024
@@ -2403,32 +2403,34 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 #endif
 constexpr int kPoolK = RT_POOL_K;          // path slots per wave
 constexpr int kBlockPool = RT_POOL_BLOCK;  // persistent workgroup size
-constexpr int kPoolGroups = 4;             // 16-byte groups per slot (below)
+constexpr int kPoolGroups = 3;             // 16-byte groups per slot, plus one 8-byte group (below)
 static_assert(kPoolK >= kWave && kPoolK <= 256, "pool slots: one full wave, u8 queue entries");
 // Per wave: slot state as [group][slot] float4, then the A queue (a ring) and the D queue
 // (u8 slot indices; with RT_POOL_DSPLIT two stacks in one array: cosine-branch paths from
 // the bottom, light-branch paths from the top - together at most kPoolK entries).
-// 64 bytes per slot (more slots per wave fill more trips: 64 / 80 / 96 slots ran Cornell in
-// 21.7 / 17.7 / 16.1 ms, profiles/r02/poolsize/):
-//   g0 {rng lo, rng hi, meta, hf}   meta = (phase + 2) | lambert material << 8 (D only),
-//                                   phase: bounces so far (>= 0), PH_NEW or PH_ITEM;
-//                                   hf = h | planar << 30 | front << 31 (D only)
+// 56 bytes per slot (more slots per wave fill more trips: 64 / 80 / 96 slots ran Cornell in
+// 21.7 / 17.7 / 16.1 ms, profiles/r02/poolsize/; 119 / 134 / 152 slots followed):
+//   g0 {rng lo, rng hi, meta, hs}   meta = (phase + 2) | log2(item chunk) << 8 | lambert material << 11
+//                                   (D only), phase: bounces so far (>= 0), PH_NEW or PH_ITEM;
+//                                   hs = h | planar << 14 | front << 15 (D only) | s << 16
 //   g1 {o (hit point p when queued for D), slot}
-//   g2 {d (the face normal when queued for D), s | s_end << 16}
-//   g3 {T, i | j << 16}
-// The D stage reads the Lambertian albedo (the scatter's attenuation) from the material
-// table. Host gates: spp <= 65535, depth <= 250, materials < 2^24.
-constexpr size_t kPoolWaveBytes = ((size_t)kPoolK * kPoolGroups * 16 + 2 * kPoolK + 15) / 16 * 16;
-__device__ __forceinline__ float pool_meta(int phase, int mat) {
-    return __uint_as_float((uint32_t)((phase + 2) & 0xff) | ((uint32_t)mat << 8));
+//   g2 {d (the face normal when queued for D), T.x}
+//   g3 {T.y, T.z}                    (the 8-byte group)
+// The item's end is the next multiple of its (power-of-two) chunk, the pixel comes from the
+// slot (item_pixel), and the D stage reads the Lambertian albedo (the scatter's attenuation)
+// from the material table. Host gates: spp <= 65535, depth <= 250, materials < 2^21,
+// primitives < 2^14, power-of-two chunks.
+constexpr size_t kPoolWaveBytes = ((size_t)kPoolK * (kPoolGroups * 16 + 8) + 2 * kPoolK + 15) / 16 * 16;
+__device__ __forceinline__ float pool_meta(int phase, int clog2, int mat) {
+    return __uint_as_float((uint32_t)((phase + 2) & 0xff) | ((uint32_t)clog2 << 8) | ((uint32_t)mat << 11));
 }
 __device__ __forceinline__ int meta_phase(float m) { return (int)(__float_as_uint(m) & 0xffu) - 2; }
-__device__ __forceinline__ int meta_mat(float m) { return (int)(__float_as_uint(m) >> 8); }
-__device__ __forceinline__ float pool_ss(int s, int s_end) {
-    return __uint_as_float((uint32_t)s | ((uint32_t)s_end << 16));
-}
-__device__ __forceinline__ int ss_s(float v) { return (int)(__float_as_uint(v) & 0xffffu); }
-__device__ __forceinline__ int ss_end(float v) { return (int)(__float_as_uint(v) >> 16); }
+__device__ __forceinline__ int meta_clog2(float m) { return (int)((__float_as_uint(m) >> 8) & 7u); }
+__device__ __forceinline__ int meta_mat(float m) { return (int)(__float_as_uint(m) >> 11); }
+__device__ __forceinline__ float pool_hs(int hf16, int s) { return __uint_as_float(((uint32_t)hf16 & 0xffffu) | ((uint32_t)s << 16)); }
+__device__ __forceinline__ int hs_s(float v) { return (int)(__float_as_uint(v) >> 16); }
+__device__ __forceinline__ int hs_hf(float v) { return (int)(__float_as_uint(v) & 0xffffu); }
+__device__ __forceinline__ int item_end(int s, int clog2) { return ((s >> clog2) + 1) << clog2; }
 constexpr size_t pool_lds_bytes() { return (size_t)(kBlockPool / kWave) * kPoolWaveBytes; }
 enum : int { PH_NEW = -1, PH_ITEM = -2 };  // next sample's path to start / no work item
 
@@ -2467,7 +2469,8 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kStackStride + threadIdx.x;
     char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * kPoolWaveBytes;
     float4* G = reinterpret_cast<float4*>(wpool);  // group q of slot k: G[q * kPoolK + k]
-    uint8_t* qa = reinterpret_cast<uint8_t*>(wpool + (size_t)kPoolK * kPoolGroups * 16);
+    float2* G3 = reinterpret_cast<float2*>(wpool + (size_t)kPoolK * kPoolGroups * 16);  // the 8-byte group
+    uint8_t* qa = reinterpret_cast<uint8_t*>(wpool + (size_t)kPoolK * (kPoolGroups * 16 + 8));
     uint8_t* qd = qa + kPoolK;
     const int endX = min(reg.x + reg.width, C0.width);
     const int endY = min(reg.y + reg.height, C0.height);
@@ -2482,7 +2485,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
 
     for (int k = lane; k < kPoolK; k += kWave) {
         qa[k] = (uint8_t)k;
-        G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0), 0.f);
+        G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
     }
     int a_head = 0, a_cnt = kPoolK, d_head = 0, d_cnt = 0;  // wave-uniform queue state
     int dl_cnt = 0;  // RT_POOL_DSPLIT: light-branch stack (d_cnt: cosine-branch stack)
@@ -2528,37 +2531,38 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 d_cnt -= n;
             }
             if (k >= 0) {
-                const float4 g0 = G[k], g1 = G[kPoolK + k], g2 = G[2 * kPoolK + k], g3 = G[3 * kPoolK + k];
+                const float4 g0 = G[k], g1 = G[kPoolK + k], g2 = G[2 * kPoolK + k];
+                const float2 g3 = G3[k];
                 Path<false> P;
                 P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
                 P.bounces = meta_phase(g0.z);
                 P.em_n = 0;
                 P.o = V3{g1.x, g1.y, g1.z};
                 P.d = V3{g2.x, g2.y, g2.z};
-                P.T = V3{g3.x, g3.y, g3.z};
-                const int hf = __float_as_int(g0.w);
-                const int h = hf & 0x3fffffff;
+                P.T = V3{g2.w, g3.x, g3.y};
+                const int hf = hs_hf(g0.w);
+                const int h = hf & 0x3fff;
+                const bool planar = (hf >> 14) & 1, front = (hf >> 15) & 1;
                 const V3 att = ld3(S.mats[meta_mat(g0.z)].color);  // the Lambertian scatter's attenuation
-                const int s_end = ss_end(g2.w), slot = __float_as_int(g1.w);
-                int s = ss_s(g2.w);
+                const int clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w);
+                int s = hs_s(g0.w);
+                const int s_end = item_end(s, clog2);
                 phase = P.bounces;
                 const RtCamera& C = cam_opaque();
                 const bool dterm =
-                    !RT_POOL_DSPLIT ? shade_diffuse<Real, false, false, PP, 0>(S, C, P, h, (hf >> 30) & 1, hf < 0,
-                                                                               P.o, P.d, att, cnt, pf)
-                    : dtop ? shade_diffuse<Real, false, false, PP, 2>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
-                                                                      att, cnt, pf)
-                           : shade_diffuse<Real, false, false, PP, 1>(S, C, P, h, (hf >> 30) & 1, hf < 0, P.o, P.d,
-                                                                      att, cnt, pf);
+                    !RT_POOL_DSPLIT ? shade_diffuse<Real, false, false, PP, 0>(S, C, P, h, planar, front, P.o, P.d, att,
+                                                                               cnt, pf)
+                    : dtop ? shade_diffuse<Real, false, false, PP, 2>(S, C, P, h, planar, front, P.o, P.d, att, cnt, pf)
+                           : shade_diffuse<Real, false, false, PP, 1>(S, C, P, h, planar, front, P.o, P.d, att, cnt, pf);
                 if (dterm) {
                     // mixture value cut-off: the level's emission (as computed at the hit: T is unchanged)
                     const V3 c = mulv(ld3(S.mats[S.prims[h].mat].emitted), P.T);
                     phase = record(c, P.bounces, slot, s, s_end);
                 }
                 G[k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
-                                   pool_meta(phase, 0), 0.f);
-                G[2 * kPoolK + k] = make_float4(P.d.x, P.d.y, P.d.z, pool_ss(s, s_end));
-                G[3 * kPoolK + k] = make_float4(P.T.x, P.T.y, P.T.z, g3.w);
+                                   pool_meta(phase, clog2, 0), pool_hs(0, s));
+                G[2 * kPoolK + k] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
+                G3[k] = make_float2(P.T.y, P.T.z);
             }
             if (RT_POOL_ASPLIT) {
                 stack_push(qa, false, an_cnt, k >= 0 && phase < 0, k);
@@ -2581,15 +2585,16 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 a_head = pool_ring(a_head + n);
                 a_cnt -= n;
             }
-            float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0), 0.f), g1 = g0, g2 = g0, g3 = g0;
+            float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f), g1 = g0, g2 = g0;
+            float2 g3 = make_float2(0.f, 0.f);
             if (k >= 0) {
                 g0 = G[k];
                 g1 = G[kPoolK + k];
                 g2 = G[2 * kPoolK + k];
-                g3 = G[3 * kPoolK + k];
+                g3 = G3[k];
             }
-            int phase = meta_phase(g0.z), s_end = ss_end(g2.w), slot = __float_as_int(g1.w);
-            int s = ss_s(g2.w), ij = __float_as_int(g3.w);
+            int phase = meta_phase(g0.z), clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w);
+            int s = hs_s(g0.w);
             // work items for slots without one (the chunked kernel's guided hand-out)
             const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
             if (need != 0ull && !exhausted) {
@@ -2613,8 +2618,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                         if (i < endX && j < endY) {
                             slot = tl * 64 + l;
                             s = s1;
-                            s_end = e1;
-                            ij = i | (j << 16);
+                            clog2 = __builtin_ctz((uint32_t)(e1 - s1));  // power-of-two, aligned chunks
                             phase = PH_NEW;
                         }
                     }
@@ -2627,14 +2631,15 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 const RtCamera& C = cam_opaque();
                 Path<false> P;
                 if (phase == PH_NEW) {
-                    const int i = ij & 0xffff, j = ij >> 16;
+                    int i, j;  // the slot's pixel (the hand-out's item_pixel)
+                    item_pixel(reg, tiles_x, rtx, sb.tile0 + (slot >> 6), slot & 63, i, j);
                     path_begin<Real, false>(C, P, pixel_center<Real>(C, i, j),
                                             (uint32_t)j * (uint32_t)C.width + (uint32_t)i, (uint32_t)s);
                 } else {
                     P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
                     P.o = V3{g1.x, g1.y, g1.z};
                     P.d = V3{g2.x, g2.y, g2.z};
-                    P.T = V3{g3.x, g3.y, g3.z};
+                    P.T = V3{g2.w, g3.x, g3.y};
                     P.bounces = phase;
                     P.em_n = 0;
                 }
@@ -2673,7 +2678,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                             } else {
                                 to_d = true;
                                 P.d = nrm;  // queued for D: g2 carries the face normal
-                                hf = h | (planar ? (1 << 30) : 0) | (front ? (int)0x80000000 : 0);
+                                hf = h | (planar ? (1 << 14) : 0) | (front ? (1 << 15) : 0);
                                 if (RT_POOL_DSPLIT) {  // shade_diffuse's first draw and branch, ahead
                                     uint64_t r = P.rng;
                                     const Real u0 = uniform<Real>(r);
@@ -2684,20 +2689,20 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                         }
                     }
                 }
-                phase = term ? record(c, P.bounces, slot, s, s_end) : P.bounces;
+                phase = term ? record(c, P.bounces, slot, s, item_end(s, clog2)) : P.bounces;
                 g0 = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
-                                 pool_meta(phase, to_d ? dmat : 0), __int_as_float(hf));
+                                 pool_meta(phase, clog2, to_d ? dmat : 0), pool_hs(to_d ? hf : 0, s));
                 g1 = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
-                g2 = make_float4(P.d.x, P.d.y, P.d.z, pool_ss(s, s_end));
-                g3 = make_float4(P.T.x, P.T.y, P.T.z, __int_as_float(ij));
+                g2 = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
+                g3 = make_float2(P.T.y, P.T.z);
             } else if (keep) {  // a slot still waiting for a work item
-                g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0), 0.f);
+                g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
             }
             if (keep) {
                 G[k] = g0;
                 G[kPoolK + k] = g1;
                 G[2 * kPoolK + k] = g2;
-                G[3 * kPoolK + k] = g3;
+                G3[k] = g3;
             }
             if (RT_POOL_ASPLIT) {
                 stack_push(qa, false, an_cnt, keep && !to_d && phase < 0, k);

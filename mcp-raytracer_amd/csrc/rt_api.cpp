@@ -363,7 +363,8 @@ struct rt_camera {
         // 14.12 vs 14.23 ms, profiles/r02/asplit/). RT_AMD_POOL_KERNEL=0/1 overrides.
         S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
         v.pool = !v.emit && (count == 0 || (RT_POOL_PROF && count == 2 && prec == PREC_REF)) && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
-                 C.n_samples <= 65535 && C.depth <= 250 && build.mats.size() < (1u << 24) &&  // 64-byte slot fields
+                 C.n_samples <= 65535 && C.depth <= 250 && build.mats.size() < (1u << 21) &&  // 56-byte slot fields
+                 build.prims.size() < (1u << 14) &&
                  (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
         // guided schedule: half of the remaining samples per phase, chunks halving.
@@ -398,9 +399,12 @@ struct rt_camera {
             const double c_target = bvh ? std::sqrt(spl) / 3.0 : spl / 8.0;
             int c_auto = 1;
             while (c_auto * 2 <= c_max && c_auto * 2 <= c_target) c_auto *= 2;  // pow2 floor, in [1, c_max]
-            int s0 = 0, c = std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2)), np = 0;
+            // power-of-two chunks: items are aligned to their chunk (the pool kernel derives an
+            // item's end from its sample index)
+            auto pow2floor = [](int x) { int p = 1; while (p * 2 <= x) p *= 2; return p; };
+            int s0 = 0, c = pow2floor(std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2))), np = 0;
             if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
-                c = std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples);
+                c = pow2floor(std::max(1, std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples)));
                 const int full = C.n_samples / c;
                 sb.s0[np] = 0; sb.chunk[np] = c; sb.nch[np] = full; ++np;
                 s0 = full * c;
