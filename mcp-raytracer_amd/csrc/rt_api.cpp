@@ -391,11 +391,14 @@ struct rt_camera {
             // Trees walked from global memory (a sample costs ~150 us of a lane at config 5) cap
             // the first chunk at 4 (config 5, 4096^2 spp1024: 9617 -> 8980 ms per frame).
             const bool bvh = v.trav == TRAV_FAST;
-            const int pool_auto = v.pool ? (spl >= 256.0 ? 4 : spl >= 128.0 ? 2 : 1)
+            // (pool kernel, re-tuned at 152 slots per wave: 8 tile-chunks per atomic from 512 spl,
+            // 4 from 48, 2 from 24, first items of at most 4 samples - Cornell N=1 14.61 -> 14.43 ms,
+            // 1/2 share 7.57 -> 7.40, 1/8 share 2.57 -> 2.10 ms; profiles/r02/sched/)
+            const int pool_auto = v.pool ? (spl >= 512.0 ? 8 : spl >= 48.0 ? 4 : spl >= 24.0 ? 2 : 1)
                                  : bvh ? (spl >= 256.0 ? 4 : 2)
                                        : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
-            const int c_max = v.pool ? 8 : (bvh && g.lds_level == 0) ? 4 : 32;
+            const int c_max = v.pool ? 4 : (bvh && g.lds_level == 0) ? 4 : 32;
             const double c_target = bvh ? std::sqrt(spl) / 3.0 : spl / 8.0;
             int c_auto = 1;
             while (c_auto * 2 <= c_max && c_auto * 2 <= c_target) c_auto *= 2;  // pow2 floor, in [1, c_max]
