@@ -408,6 +408,26 @@ def test_pool_kernel_equals_chunked_kernel(rt, gpu, case, monkeypatch):
         assert sa.pixels == sb.pixels and sa.samples == sb.samples and sa.bounces == sb.bounces
 
 
+@pytest.mark.parametrize("ro,kernel", [
+    ({"width": 24, "samples": 3, "depth": 250}, "pool"),        # deepest path a slot's phase byte holds
+    ({"width": 24, "samples": 3, "depth": 251}, "chunked"),     # past it: host falls back
+    ({"width": 4, "samples": 65535, "depth": 4}, "pool"),       # largest sample index a slot holds
+    ({"width": 4, "samples": 65536, "depth": 4}, "chunked"),
+])
+def test_pool_host_gates_fall_back_bit_exact(rt, oracle, gpu, ro, kernel):
+    """The pool kernel packs the bounce phase into 8 bits and the sample index
+    into 16 (pt_kernel.hpp pool_meta / pool_hs); rt_api.cpp gates it on
+    depth <= 250 and spp <= 65535. On each side of both gates the default path
+    picks the expected kernel and matches the oracle bit for bit."""
+    sd = rt.generate_scene_data({"type": "cornell"})
+    ro = {**ro, "aspect": 1, **NOADAPT}
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == kernel
+    orc = oracle.render(sd, ro, threads=8)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"gate {ro} -> {kernel}")
+    assert_stats_identical(st, orc["stats"])
+
+
 def _tiny_scene(n):
     objs = [{"type": "sphere", "pos": [0.9 * k - 0.9, 0.3 * (k % 2), -0.2 * k], "r": 0.45, "material": "m"}
             for k in range(n)]
