@@ -3,6 +3,8 @@
 combination of environment overrides, path-kernel ms from HIP events (median of 4).
 
     SWEEP_VARS="RT_AMD_READY=32,48,56 RT_AMD_REFILL=1,4" python tools/env_sweep.py spheres100k
+
+SWEEP_TG=N renders rank 0's share (tile group 0 of N) instead of the whole frame.
 """
 import itertools
 import json
@@ -34,6 +36,7 @@ def main():
     for spec in os.environ.get("SWEEP_VARS", "RT_AMD_READY=48").split():
         k, vals = spec.split("=", 1)
         axes.append([(k, v) for v in vals.split(",")])
+    tg = int(os.environ.get("SWEEP_TG", "1"))
     ref = None
     for combo in itertools.product(*axes):
         for k, v in combo:
@@ -43,13 +46,13 @@ def main():
                 os.environ[k] = v
         kt = []
         for r in range(6):
-            cam.render_device(rgb_ptr=frame.data_ptr(), stream=s)
+            cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=0, tile_groups=tg, stream=s)
             if r >= 2:
                 kt.append(sum(cam.kernel_times()))
         torch.cuda.synchronize()
         img = frame.cpu().numpy()
         ref = img if ref is None else ref
-        print(json.dumps({"scene": scene, **dict(combo), "ms": round(float(np.median(kt)), 3),
+        print(json.dumps({"scene": scene, "tile_groups": tg, **dict(combo), "ms": round(float(np.median(kt)), 3),
                           "same_image": bool((img == ref).all()), "kernel": cam.last_kernel()}), flush=True)
 
 
