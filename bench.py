@@ -55,7 +55,10 @@ def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def metric_for(scene: str, W: int, H: int, spp: int, depth: int) -> str:
+def metric_for(scene: str, W: int, H: int, spp: int, depth: int, adaptive: bool = False) -> str:
+    if adaptive:
+        return (f"Msamples/sec (traced samples/s, adaptive aTolerance=0.05 aBatch=10) {SCENES[scene][2]} "
+                f"{W}×{H} spp≤{spp} depth={depth}")
     if (scene, W, H, spp, depth) == ("cornell", 800, 800, 256, 16):
         return HEADLINE_METRIC
     return f"Msamples/sec (w×h×spp/s) {SCENES[scene][2]} {W}×{H} spp={spp} depth={depth}"
@@ -156,6 +159,9 @@ def parse_args(argv):
                     help="closest-hit strategy (all bit-identical; auto = brute force up to 16 primitives)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting launch (no work_rate)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle rows check of the timed frame")
+    ap.add_argument("--adaptive", action="store_true",
+                    help="adaptive sampling with the reference's defaults (aTolerance 0.05, aBatch 10)")
     ap.add_argument("--count-sub", type=int, default=0,
                     help="tile subsample of the work-counting launch (0 = auto: 16 above 1000 objects)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
@@ -260,17 +266,23 @@ def main(argv=None):
 
     cfg, extra, _ = SCENES[args.scene]
     scene_data = rt.generate_scene_data(cfg)
-    ropts = {"width": args.width, "samples": args.spp, "depth": args.depth, "aTolerance": 0,
+    # --adaptive: the reference's default RenderOptions (aTolerance 0.05, aBatch 10;
+    # src/camera.ts:77-78), which every reference caller keeps on
+    adapt = {"aTolerance": 0.05, "aBatch": 10} if args.adaptive else {"aTolerance": 0}
+    ropts = {"width": args.width, "samples": args.spp, "depth": args.depth, **adapt,
              "seed": args.seed, "precision": args.precision, "traversal": args.traversal, **extra}
     cam = rt.create_camera_from_scene_data(scene_data, ropts)
     W, H = cam.image_width, cam.image_height
     frame = torch.zeros((H, W, 3), dtype=torch.uint8, device=dev)
+    # t_render ends with the frame on host rank 0 - every timed step
+    # copies rank 0's u8 frame into this pinned buffer
+    host_frame = torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) if rank == 0 else None
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     region = (0, 0, W, H)
-    n_px = rtd.slab_tiles(region, world) * rtd.TILE_PIXELS
-    slab = torch.zeros((n_px, 3), dtype=torch.uint8, device=dev) if world > 1 else None
-    gathered = torch.zeros((world, n_px, 3), dtype=torch.uint8, device=dev) if world > 1 and rank == 0 else None
+    n_slab = rtd.slab_pixels(region, world)  # this rank's tiles + the spare tile carrying its stats words
+    slab = torch.zeros((n_slab, 3), dtype=torch.uint8, device=dev) if world > 1 else None
+    gathered = torch.zeros((world, n_slab, 3), dtype=torch.uint8, device=dev) if world > 1 and rank == 0 else None
     log(f"rank {rank}/{world}: {args.scene} {W}x{H} spp={args.spp} depth={args.depth} build {rt.build_id()}")
 
     # Algorithmic work of this rank's launch: the node / primitive /
@@ -294,6 +306,8 @@ def main(argv=None):
             cam.render_device(rgb_ptr=frame.data_ptr(), stream=sptr)
         else:
             rtd.render_frame(cam, frame, rank, world, stream=sptr, slab=slab, gathered=gathered)
+        if rank == 0:
+            host_frame.copy_(frame, non_blocking=True)  # D2H on the same stream, inside the timed step
 
     # this rank's share (untimed): pixels and samples per launch
     st, _ = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr,
@@ -338,20 +352,33 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
 
+    # Untimed: the same frame again with its fp32 radiance (assembled over the ranks
+    # like the timed frames) and the merged RenderStats, for the checks below.
+    radiance = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+    timed_rgb = host_frame.numpy().copy() if rank == 0 else None
+    res = rtd.render_frame(cam, frame, rank, world, stream=sptr, radiance=radiance, stats=True)
+    torch.cuda.synchronize()
     frame_check = None
     if args.check:
-        step()  # a fresh assembled frame
-        torch.cuda.synchronize()
         if rank == 0:
             single = torch.zeros_like(frame)
-            cam.render_device(rgb_ptr=single.data_ptr(), stream=sptr, synchronize=True)
-            frame_check = bool(torch.equal(single, frame))
-            log(f"frame check (assembled == single launch): {frame_check}")
+            st1, _ = cam.render_device(rgb_ptr=single.data_ptr(), stream=sptr, synchronize=True)
+            frame_check = bool(torch.equal(single, frame)) and _stats_equal(res[1], st1)
+            log(f"frame check (assembled frame and merged stats == single launch): {frame_check}")
+    parity = None
+    if rank == 0 and not args.no_parity:
+        parity = parity_check(scene_data, ropts, args, timed_rgb, frame.cpu().numpy(), radiance.cpu().numpy(),
+                              res[1])
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
-        samples_per_step = W * H * args.spp
+        # samples traced per frame (merged over the ranks): W*H*spp at fixed spp; fewer
+        # with adaptive sampling, where pixels stop once converged
+        samples_per_step = int(res[1].samples["total"])
         value = samples_per_step * args.steps / elapsed / 1e6
-        key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n{world}"
+        key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n{world}" + \
+            ("_adaptive" if args.adaptive else "")
         rl = roofline(key, rt.build_id(), my_samples, kernel_ms, counters, my_pixels)
         rl.update({"kernel": kernel_name, "accum_kernel_ms": round(accum_ms, 4), "passes": passes,
                    "count_subsample": sub})
@@ -361,7 +388,7 @@ def main(argv=None):
             cpu = cpu_baseline(scene_data, {k: v for k, v in ropts.items() if k not in ("precision", "traversal")},
                                W, H, args.spp)
         line = {
-            "metric": metric_for(args.scene, W, H, args.spp, args.depth), "value": round(value, 3),
+            "metric": metric_for(args.scene, W, H, args.spp, args.depth, args.adaptive), "value": round(value, 3),
             "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -370,21 +397,102 @@ def main(argv=None):
                     f"{args.seed:#x}; no datasets",
             "config": {"workload": f"{args.scene} {W}x{H} spp={args.spp} depth={args.depth}",
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "depth": args.depth,
-                       "precision": args.precision, "adaptive": False,
+                       "precision": args.precision, "adaptive": adapt if args.adaptive else False,
+                       "samples_per_frame": samples_per_step,
                        "traversal": ["fast", "reference", "brute"][cam.info["traversal"]],
                        "kernel": KERNEL_DESC.get(kind, "sequential (wave per 8x8 tile)"),
                        "parallelism": f"8x8-tile interleave x{world}" +
                                       (" + RCCL gather of tile-packed slabs to rank 0" if world > 1 else "")},
             "build_id": rt.build_id(),
             **({"frame_check": frame_check} if args.check else {}),
+            "host_copy": "each timed step ends with rank 0's u8 frame copied into pinned host memory",
+            "parity": parity,
             "roofline": rl,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    rc = 0
+    if rank == 0 and parity is not None and not parity["ok"]:
+        log("PARITY FAILURE: the timed frame differs from the oracle")
+        rc = 3
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return rc
+
+
+def _stats_equal(a, b) -> bool:
+    return (a.pixels == b.pixels and all(a.samples[k] == b.samples[k] for k in ("total", "min", "max"))
+            and all(a.bounces[k] == b.bounces[k] for k in ("total", "min", "max")))
+
+
+def parity_check(scene_data, ropts, args, timed_rgb, rgb, rad, stats, row_budget_s=4.0):
+    """Driver-observable parity (after the timed region, never inside it): rows of
+    the frame chosen from the seed, re-rendered by the CPU oracle (same seed, same
+    precision mode) and compared bit for bit - u8 of the LAST TIMED frame as it
+    reached host memory, and the fp32 radiance of an untimed re-render whose u8
+    must equal the timed frame. Rows are full rows when the oracle can render one
+    in ~row_budget_s, else a seeded segment of each. ref precision: exact; fp32:
+    SURVEY.md §8c's tolerance (>= 99 % of pixels within 1e-3 + 1e-3|c|).
+    Reference loop: src/camera.ts:388-431."""
+    import random
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+
+    pyoracle.build()
+    H, W = rgb.shape[:2]
+    o_ro = {k: v for k, v in ropts.items() if k not in ("precision", "traversal")}
+    rnd = random.Random(args.seed * 7919 + W * 31 + H)
+    t_start = time.perf_counter()
+    # pilot: oracle cost per pixel on 8 pixels of the middle row
+    t0 = time.perf_counter()
+    pyoracle.render(scene_data, o_ro, region=(W // 2 - 4 if W >= 8 else 0, H // 2, min(8, W), 1),
+                    precision="ref")
+    t_px = max(time.perf_counter() - t0, 1e-4) / min(8, W)
+    cores = max(1, min(len(os.sched_getaffinity(0)), 16))
+    n_rows = min(H, 8 if t_px * W * 8 <= cores * row_budget_s else 4)
+    rows = sorted(rnd.sample(range(H), n_rows))
+    seg = min(W, max(8, int(row_budget_s / t_px)))
+    xs = [0 if seg == W else rnd.randrange(0, W - seg + 1) for _ in rows]
+
+    def one(k):
+        return pyoracle.render(scene_data, o_ro, region=(xs[k], rows[k], seg, 1), precision="ref")
+
+    with ThreadPoolExecutor(max_workers=min(cores, n_rows)) as ex:
+        outs = list(ex.map(one, range(n_rows)))
+    n_rgb = n_rad = n_px = n_tol = 0
+    for k, o in enumerate(outs):
+        j, x0 = rows[k], xs[k]
+        a_rgb, a_rad = timed_rgb[j, x0:x0 + seg], rad[j, x0:x0 + seg]
+        b_rgb, b_rad = o["rgb"][j, x0:x0 + seg], o["radiance"][j, x0:x0 + seg]
+        n_px += seg
+        n_rgb += int((a_rgb != b_rgb).any(axis=-1).sum())
+        same = (a_rad == b_rad) | (np.isnan(a_rad) & np.isnan(b_rad))
+        n_rad += int((~same).any(axis=-1).sum())
+        d = np.abs(a_rad.astype(np.float64) - b_rad)
+        n_tol += int((d <= 1e-3 + 1e-3 * np.abs(b_rad)).all(axis=-1).sum())
+    timed_eq = bool(np.array_equal(timed_rgb, rgb))
+    full = stats.pixels == W * H and (stats.samples["total"] == W * H * args.spp if not ropts.get("aTolerance")
+                                      else 0 < stats.samples["total"] <= W * H * args.spp)
+    if args.precision == "ref":
+        ok = n_rgb == 0 and n_rad == 0 and timed_eq and bool(full)
+        rule = "bit-exact (u8 and fp32 radiance)"
+    else:
+        ok = n_tol >= 0.99 * n_px and timed_eq and bool(full)
+        rule = "SURVEY.md §8c: >= 99 % of pixels within 1e-3 + 1e-3|c|"
+    out = {"ok": ok, "rule": rule, "rows": rows, "x": xs if seg < W else 0, "width": seg,
+           "pixels_checked": n_px, "pixels_differing_rgb": n_rgb, "pixels_differing_radiance": n_rad,
+           "pixels_within_tolerance": n_tol, "timed_frame_equals_rerender": timed_eq,
+           "stats": {"pixels": stats.pixels, "samples": stats.samples["total"], "bounces": stats.bounces["total"],
+                     "bounces_max": stats.bounces["max"]},
+           "oracle": f"oracle/oracle.cpp ref precision, {min(cores, n_rows)} threads",
+           "seconds": round(time.perf_counter() - t_start, 2)}
+    log(f"parity: {n_px} px on rows {rows}: rgb {n_rgb}, radiance {n_rad} differing; timed == rerender {timed_eq}")
+    return out
 
 
 def stub_main(args) -> int:

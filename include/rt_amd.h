@@ -176,6 +176,15 @@ int rt_device_count(int32_t* count);
  * sequential kernel). Waits for that call's events. */
 int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms);
 
+/* RenderStats words of the most recent render, queued on `stream` as a
+ * device-to-device copy into `dst` (DEVICE, 8 u64): pixels, samples total,
+ * samples min (~0 = none), samples max, bounces total, bounces min (~0 = none),
+ * bounces max, error flags. Multi-GPU ranks ship these beside their slab so rank
+ * 0 can merge them as RenderStats.merge does (src/render-utils/renderStats.ts:
+ * 42-64, called from src/raytracer.ts:86-89) without a host round trip. */
+#define RT_STATS_WORDS 8
+int rt_camera_stats_words(rt_camera* cam, uint64_t* dst, void* stream);
+
 /* Number of chunked-kernel passes of the most recent render (0 before any; the
  * sequential kernel counts as one). Passes split the per-sample record buffer. */
 int rt_camera_pass_count(rt_camera* cam, int32_t* passes);

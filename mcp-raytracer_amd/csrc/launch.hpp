@@ -25,6 +25,12 @@ struct LaunchGeom {
 constexpr int kLdsSceneMaxBytes = 152 * 1024;
 // Static LDS of the chunked / pool kernels (the phase table), beside the dynamic allocation.
 constexpr size_t kStaticLdsBytes = 512;
+// ... plus the per-wave section timers of the diagnostic variants: every kernel of a
+// count == 2 launch, and every pool kernel of an RT_POOL_PROF build.
+inline size_t static_lds_bytes(int count, bool pool) {
+    const bool prof = count == 2 || (pool && RT_POOL_PROF);
+    return kStaticLdsBytes + (prof ? (size_t)kProfWaves * kProfSlot * sizeof(unsigned long long) : 0);
+}
 
 struct KernelVariant {
     bool emit;   // emission stack (a scattering material emits)

@@ -1328,13 +1328,15 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
         cnt[CT_CAND2] += __popc(mask) >= 2 ? 1u : 0u;
     }
     while (mask != 0u) {
-        // nearest remaining candidate (a NaN bound is never skipped: it is tested exactly)
+        // nearest remaining candidate. A NaN bound orders first (as if -inf): it is
+        // selected before any finite bound and `lb > thi` is false for it, so it is
+        // always tested exactly and never ends the loop early.
         int kb = __builtin_ctz(mask);
         float lb = lot_load(lot[kb * kStackStride]);
         for (uint32_t m = mask & (mask - 1u); m != 0u; m &= m - 1u) {
             const int k = __builtin_ctz(m);
             const float l = lot_load(lot[k * kStackStride]);
-            if (l < lb) {
+            if ((l < lb || l != l) && lb == lb) {
                 lb = l;
                 kb = k;
             }
@@ -2439,6 +2441,8 @@ static_assert(kPoolK >= kWave && kPoolK <= 256, "pool slots: one full wave, u8 q
 // from the material table. Host gates: spp <= 65535, depth <= 250, materials < 2^21,
 // primitives < 2^14, power-of-two chunks.
 constexpr size_t kPoolWaveBytes = ((size_t)kPoolK * (kPoolGroups * 16 + 8) + 2 * kPoolK + 15) / 16 * 16;
+constexpr int kPoolClog2Bits = 3;  // log2(item chunk) field of the slot meta word
+constexpr int kPoolMaxChunk = 1 << ((1 << kPoolClog2Bits) - 1);  // 128 samples
 __device__ __forceinline__ float pool_meta(int phase, int clog2, int mat) {
     return __uint_as_float((uint32_t)((phase + 2) & 0xff) | ((uint32_t)clog2 << 8) | ((uint32_t)mat << 11));
 }

@@ -22,6 +22,8 @@
 
 using namespace rt;
 
+static_assert(ST_WORDS == RT_STATS_WORDS, "rt_camera_stats_words layout");
+
 #ifndef RT_BUILD_ID
 #define RT_BUILD_ID "unhashed"
 #endif
@@ -322,7 +324,7 @@ struct rt_camera {
         // profiles/r02/defer/). RT_AMD_DEFER=0/1 overrides.
         v.defer = v.trav == TRAV_FAST &&
                   env_flag("RT_AMD_DEFER", g.lds_level >= 1 && C.n_prims >= 100);
-        if (g.lds_bytes + kStaticLdsBytes > (size_t)lds_max)
+        if (g.lds_bytes + static_lds_bytes(count, false) > (size_t)lds_max)
             throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile, packed ? 1 : 0};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
@@ -365,7 +367,7 @@ struct rt_camera {
         v.pool = !v.emit && (count == 0 || (RT_POOL_PROF && count == 2 && prec == PREC_REF)) && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
                  C.n_samples <= 65535 && C.depth <= 250 && build.mats.size() < (1u << 21) &&  // 56-byte slot fields
                  build.prims.size() < (1u << 14) &&
-                 (size_t)S.lds_pool_off + pool_lds_bytes() + kStaticLdsBytes <= (size_t)lds_max &&
+                 (size_t)S.lds_pool_off + pool_lds_bytes() + static_lds_bytes(count, true) <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
         // guided schedule: half of the remaining samples per phase, chunks halving.
         // First-phase chunk from the samples per resident lane: an item is the
@@ -427,6 +429,11 @@ struct rt_camera {
                 c /= 2;
             }
             sb.n_phases = np;
+            // the pool kernel keeps log2(item chunk) in a 3-bit slot field (pool_meta): chunks
+            // of more than kPoolMaxChunk samples (RT_AMD_CHUNK overrides) take the chunked kernel
+            if (v.pool)
+                for (int p = 0; p < np; ++p)
+                    if (sb.chunk[p] > kPoolMaxChunk) v.pool = false;
             int covered = 0;
             for (int p = 0; p < np; ++p) {
                 if (sb.s0[p] != covered) throw std::runtime_error("guided schedule: gap");
@@ -801,6 +808,23 @@ int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms) {
             }
         }
         return RT_OK;
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_DEVICE, e.what());
+    }
+}
+
+int rt_camera_stats_words(rt_camera* cam, uint64_t* dst, void* stream) {
+    if (!cam || !dst) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    try {
+        if (cam->device < 0 || !cam->d_stats) throw std::invalid_argument("rt_camera_stats_words: no render yet");
+        // the ST_WORDS words sit kStatStride apart (one 128-B line each); dst gets them packed
+        hip_check(hipMemcpy2DAsync(dst, sizeof(uint64_t), cam->d_stats, kStatStride * sizeof(unsigned long long),
+                                   sizeof(uint64_t), ST_WORDS, hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                  "hipMemcpy2DAsync(stats)");
+        return RT_OK;
+    } catch (const std::invalid_argument& e) {
+        return set_error(RT_ERR_INVALID, e.what());
     } catch (const std::exception& e) {
         return set_error(RT_ERR_DEVICE, e.what());
     }

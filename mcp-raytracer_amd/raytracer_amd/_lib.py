@@ -24,6 +24,7 @@ CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_
             "bounces", "diffuse", "samples", "rays", "exact", "exact_wave", "cand0", "cand2", "exact2"]
 PR_NAMES = ["newpath", "rr", "hit", "miss", "hitrec", "scatter", "sample", "pdf", "acc", "tile", "loop", "trips"]
 COUNTER_WORDS = 64
+STATS_WORDS = 8  # RT_STATS_WORDS: pixels, samples, smin, smax, bounces, bmin, bmax, error
 
 
 class RtRegion(C.Structure):
@@ -86,6 +87,7 @@ _SIGS = {
     "rt_debug_math": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "rt_camera_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "rt_camera_stats_words": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_camera_pass_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rt_camera_last_kernel": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rt_camera_release_device": (C.c_int, [C.c_void_p]),

@@ -191,6 +191,11 @@ class Camera:
         _lib.check(self._lib.rt_camera_kernel_times(self._h, C.byref(a), C.byref(b)))
         return float(a.value), float(b.value)
 
+    def stats_words(self, dst_ptr: int, stream=None) -> None:
+        """Queue a copy of the last render's 8 RenderStats words (u64) to the
+        device address `dst_ptr` on `stream` (rt_camera_stats_words)."""
+        _lib.check(self._lib.rt_camera_stats_words(self._h, C.c_void_p(dst_ptr), C.c_void_p(stream)))
+
     def pass_count(self) -> int:
         """Chunked-kernel passes of the last render (rt_camera_pass_count)."""
         n = C.c_int32()

@@ -24,3 +24,34 @@ def test_cpu_baseline_contract(rt):
     if mc is not None:  # hosts with more than one usable core
         assert mc["cores"] > 1 and mc["value"] > 0 and mc["unit"] == "Msamples/s"
         assert isinstance(mc["cpu"], str) and mc["cpu"]
+
+
+def test_parity_check_accepts_the_oracle_frame_and_flags_one_pixel(rt, oracle):
+    """bench.py's driver-observable parity leg on the CPU: fed the oracle's own
+    frame it reports 0 / 0 differing pixels; one changed radiance value or u8
+    byte on a checked row fails it; a timed frame that differs from the re-render
+    fails it too."""
+    from types import SimpleNamespace
+
+    import bench
+    from raytracer_amd.camera import RenderStats
+
+    sd = rt.generate_scene_data({"type": "spheres"})
+    ro = {"width": 40, "aspect": 1, "samples": 4, "depth": 4, "aTolerance": 0, "seed": 0x5EED}
+    orc = oracle.render(sd, ro)
+    fs = orc["stats"]
+    st = RenderStats(pixels=fs["pixels"], samples=dict(fs["samples"]), bounces=dict(fs["bounces"]))
+    args = SimpleNamespace(seed=0x5EED, spp=4, precision="ref")
+    rgb, rad = orc["rgb"].copy(), orc["radiance"].copy()
+    p = bench.parity_check(sd, {**ro, "precision": "ref", "traversal": "auto"}, args, rgb, rgb, rad, st)
+    assert p["ok"] and p["pixels_differing_rgb"] == 0 and p["pixels_differing_radiance"] == 0
+    assert p["pixels_checked"] == 40 * len(p["rows"]) and len(p["rows"]) >= 4
+    j = p["rows"][1]
+    bad = rad.copy()
+    bad[j, 7, 1] = bad[j, 7, 1] * 1.0000001 + 1e-7
+    q = bench.parity_check(sd, ro, args, rgb, rgb, bad, st)
+    assert not q["ok"] and q["pixels_differing_radiance"] == 1 and q["rows"] == p["rows"]
+    other = rgb.copy()
+    other[(j + 1) % 40 if (j + 1) % 40 not in p["rows"] else 0, 0, 0] ^= 1
+    r = bench.parity_check(sd, ro, args, other, rgb, rad, st)
+    assert not r["ok"] and not r["timed_frame_equals_rerender"]

@@ -153,3 +153,72 @@ def test_bench_metric_names_the_workload():
     assert bench.metric_for("cornell", 800, 800, 256, 16) == bench.HEADLINE_METRIC
     m = bench.metric_for("spheres100k", 4096, 4096, 1024, 100)
     assert "spheres-100k" in m and "4096×4096" in m and "spp=1024" in m
+
+
+def _words_of(st):
+    """The 8 stats words (rt_camera_stats_words layout) of an oracle render's stats."""
+    none = -1  # ~0 as int64
+    s, b = st["samples"], st["bounces"]
+    return [int(st["pixels"]), int(s["total"]), none if s["min"] == float("inf") else int(s["min"]), int(s["max"]),
+            int(b["total"]), none if b["min"] == float("inf") else int(b["min"]), int(b["max"]), 0]
+
+
+def _stats_worker(rank, world, port, words, n_px, q):
+    import torch
+    import torch.distributed as dist
+    from raytracer_amd.distributed import gather_slabs, gathered_stats, stats_from_words
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a u8 slab with the spare tile: pixels (here zeros), then the stats words
+    slab = torch.zeros((n_px + 64, 3), dtype=torch.uint8)
+    slab.view(-1)[n_px * 3:n_px * 3 + 64].view(torch.int64).copy_(torch.tensor(words[rank], dtype=torch.int64))
+    g = gather_slabs(slab, world)
+    if rank == 0:
+        st = stats_from_words(gathered_stats(g, n_px).tolist())
+        q.put((st.pixels, st.samples, st.bounces))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_rank_stats_merge_equals_single_render(oracle, rt):
+    """RenderStats across ranks (RenderStats.merge, src/render-utils/renderStats.ts:
+    42-64): each rank's 8 stats words ride in its slab's spare tile through the
+    gather; rank 0's merge equals the stats of one render of the whole region.
+    Adaptive sampling makes min / max per-pixel sample counts differ by rank."""
+    import torch.multiprocessing as mp
+    sd = rt.generate_scene_data({"type": "cornell"})
+    ro = {"width": 24, "samples": 30, "depth": 6, "aTolerance": 0.05, "aBatch": 10}
+    full = oracle.render(sd, ro)
+    W, H = full["width"], full["height"]
+    parts = [oracle.render(sd, ro, region=(0, 0, W, H // 3)), oracle.render(sd, ro, region=(0, H // 3, W, H - H // 3))]
+    words = [_words_of(p["stats"]) for p in parts]
+    assert parts[0]["stats"]["samples"]["total"] != parts[1]["stats"]["samples"]["total"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, 2, port, words, 5 * 64, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    pixels, samples, bounces = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fs = full["stats"]
+    assert pixels == fs["pixels"]
+    for k in ("total", "min", "max"):
+        assert samples[k] == fs["samples"][k] and bounces[k] == fs["bounces"][k], k
+    assert samples["avg"] == fs["samples"]["total"] / fs["pixels"]
+
+
+def test_merge_stats_words_skips_empty_ranks_and_ors_errors():
+    import torch
+    from raytracer_amd.distributed import merge_stats_words, stats_from_words
+    w = torch.tensor([[10, 40, 4, 4, 90, 1, 16, 0], [0, 0, -1, 0, 0, -1, 0, 0], [6, 24, 4, 4, 30, 0, 9, 0]])
+    st = stats_from_words(merge_stats_words(w).tolist())
+    assert (st.pixels, st.samples["total"], st.samples["min"], st.samples["max"]) == (16, 64, 4, 4)
+    assert (st.bounces["total"], st.bounces["min"], st.bounces["max"]) == (120, 0, 16)
+    empty = stats_from_words(merge_stats_words(w[1:2]).tolist())
+    assert empty.samples["min"] == float("inf") and empty.bounces["min"] == float("inf")
+    w[2, 7] = 2
+    with pytest.raises(RuntimeError, match="emission stack"):
+        stats_from_words(merge_stats_words(w).tolist())

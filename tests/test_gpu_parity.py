@@ -693,20 +693,42 @@ def test_release_device_then_render_again(rt, gpu):
         assert np.array_equal(rgb, rgb2) and np.array_equal(rad, rad2) and st.bounces == st2.bounces
 
 
+PACKED_CASES = {
+    # chunked kernel, one pass
+    "rain": ({"type": "rain", "options": {"seed": 42}}, {"width": 72, "samples": 4, "depth": 8, **NOADAPT}, {},
+             "chunked"),
+    # the pool kernel's packed-index path
+    "cornell_pool": ({"type": "cornell"}, {"width": 72, "samples": 8, "depth": 8, **NOADAPT}, {}, "pool"),
+    # adaptive sampling: the sequential kernel's packed index (tile * 64 + lane)
+    "adaptive": ({"type": "cornell"}, {"width": 72, "samples": 30, "depth": 8}, {}, "sequential"),
+    # a record budget that forces several passes (the pass's tile offset in the packed index)
+    "multipass": ({"type": "rain", "options": {"seed": 42}}, {"width": 72, "samples": 64, "depth": 8, **NOADAPT},
+                  {"RT_AMD_SBUF_MB": "1"}, "chunked"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(PACKED_CASES))
 @pytest.mark.parametrize("region", [None, (3, 5, 50, 41)])
-def test_packed_slabs_unpack_to_the_frame(rt, gpu, region):
+def test_packed_slabs_unpack_to_the_frame(rt, gpu, region, case, monkeypatch):
     """The multi-GPU gather's device side: each tile group's tile-packed render
     (rt_launch.packed_tiles), stacked as the RCCL gather stacks them, unpacked by
-    rt_tiles_unpack, equals the single full-frame render (u8 and fp32)."""
+    rt_tiles_unpack, equals the single full-frame render (u8 and fp32) - for every
+    kernel's packed-index path (chunked, pool, sequential / adaptive, multi-pass)."""
     import torch
     from raytracer_amd import distributed as rtd
-    sd = rt.generate_scene_data({"type": "rain", "options": {"seed": 42}})
-    cam = rt.create_camera_from_scene_data(sd, {"width": 72, "samples": 4, "depth": 8, **NOADAPT})
+    cfg, ro, env, kernel = PACKED_CASES[case]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sd = rt.generate_scene_data(cfg)
+    cam = rt.create_camera_from_scene_data(sd, ro)
     W, H = cam.image_width, cam.image_height
     reg = rtd.clamp_region(region or (0, 0, W, H), W, H)
     full = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
     frad = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
     cam.render_device(rgb_ptr=full.data_ptr(), radiance_ptr=frad.data_ptr(), region=reg, synchronize=True)
+    assert cam.last_kernel() == kernel
+    if case == "multipass":
+        assert cam.pass_count() > 1
     for world in (1, 3, 8):
         n_px = rtd.slab_tiles(reg, world) * 64
         slabs = torch.zeros((world, n_px, 3), dtype=torch.uint8, device="cuda")

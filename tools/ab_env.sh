@@ -6,6 +6,6 @@ echo "$CFGS" | while read -r tag args; do
   [ -z "$tag" ] && continue
   echo "$ARMS" | while read -r arm envs; do
     [ -z "$arm" ] && continue
-    env $envs timeout -k 10 ${TLIM:-200} python bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu --no-count $args > $OUT/${tag}_${arm}.log 2>&1 || exit $?
+    env $envs timeout -k 10 ${TLIM:-200} python bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu --no-count --no-parity $args > $OUT/${tag}_${arm}.log 2>&1 || exit $?
   done || exit $?
 done

@@ -1,0 +1,59 @@
+#!/bin/bash
+# One parameterised GPU session runner (replaces the per-session gpu_*.sh scripts).
+# usage: bash tools/gpu_run.sh <tag> <step> [<step> ...]     (from $GRAFT_REPO_ROOT on the box)
+# steps:
+#   pytest            the -m gpu suite (per-test thread timeout)
+#   pytest:<expr>     the -m gpu suite restricted by -k <expr>
+#   bench             the default bench line (N=1 headline, CPU leg + parity)
+#   bench4            Cornell ref / spheres-500 / rain 1080p spp512 / spheres-100k spp16 (no CPU leg)
+#   fp32              Cornell in fp32 mode
+#   adaptive          Cornell 800^2 spp256 with the reference's adaptive defaults
+#   config5           BASELINE config 5 (spheres-100k 4096^2 spp1024 depth 100)
+#   prof              bench under rocprofv3 --kernel-trace --stats (csv)
+#   valu / traffic    the VALU / HBM counter passes of the bench configs (separate --pmc runs)
+#   rankshare         tools/rank_share.py for Cornell and spheres-500
+#   sections          tools/profile_sections.py (section timers of the pool kernel)
+#   bench:<args>      one extra bench line with <args> (underscores become spaces)
+# Every GPU step runs under its own time limit; the first failing step ends the script.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; shift
+O=gpurun_out/$TAG
+mkdir -p $R/$O
+cd $R
+B="python bench.py --no-cpu"
+CFGS4=("" "--scene spheres --spp 64 --depth 8" "--scene rain --width 1920 --spp 512 --depth 16" \
+       "--scene spheres100k --width 4096 --spp 16 --depth 100")
+run() {  # run <seconds> <log> <cmd...>
+  local t=$1 log=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$log 2>&1
+  local rc=$?
+  echo "$(date +%T) $log rc=$rc" >> $O/steps.txt
+  return $rc
+}
+for step in "$@"; do
+  case $step in
+    pytest) run 900 pytest_gpu.log python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    pytest:*) run 900 pytest_k.log python -u -m pytest tests -m gpu -x -v -k "${step#pytest:}" --timeout 200 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    bench) run 300 bench_default.log python bench.py || exit $? ;;
+    bench4)
+      run 200 b_cornell.log $B --steps 5 --warmup 1 || exit $?
+      run 200 b_spheres.log $B ${CFGS4[1]} --steps 5 --warmup 1 || exit $?
+      run 200 b_rain.log $B ${CFGS4[2]} --steps 3 --warmup 1 || exit $?
+      run 300 b_100k.log $B ${CFGS4[3]} --steps 2 --warmup 1 || exit $? ;;
+    fp32) run 200 b_cornell_fp32.log $B --precision fp32 --steps 5 --warmup 1 || exit $? ;;
+    adaptive) run 300 b_adaptive.log $B --adaptive --steps 3 --warmup 1 || exit $? ;;
+    config5) run 600 b_config5.log $B --scene spheres100k --width 4096 --spp 1024 --depth 100 --steps 1 --warmup 0 --no-count || exit $? ;;
+    bench:*) a=${step#bench:}; run 300 b_extra_$(echo $a | tr -c 'a-z0-9' _ | cut -c1-40).log $B ${a//_/ } || exit $? ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
+        --output-format csv -- python3 $R/bench.py --no-cpu > $R/$O/prof.log 2>&1) || exit $? ;;
+    valu) VALU_DIR=$O/valu bash tools/pmc_valu.sh "${CFGS4[@]:0:3}" "--precision fp32" || exit $? ;;
+    traffic) bash tools/pmc_traffic.sh "${CFGS4[@]:0:3}" || exit $? ;;
+    rankshare)
+      run 200 rank_share_cornell.log python tools/rank_share.py cornell || exit $?
+      run 200 rank_share_spheres.log python tools/rank_share.py spheres || exit $? ;;
+    sections) run 300 sections.log python tools/profile_sections.py || exit $? ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
+exit 0

@@ -8,5 +8,5 @@ P2="TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_s
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $P -d $O/p$i -o run --output-format csv -- python3 $R/bench.py $2 --steps 2 --warmup 0 --no-cpu --no-count > $O/p$i.log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $P -d $O/p$i -o run --output-format csv -- python3 $R/bench.py $2 --steps 2 --warmup 0 --no-cpu --no-count --no-parity > $O/p$i.log 2>&1 || exit $?
 done

@@ -2,7 +2,8 @@
 """Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_traffic.json.
 
 Per configuration: the dominant kernel's (pt_pool_kernel, else pt_chunk_kernel, else
-pt_render_kernel; product build INSTR=0) counters averaged over its dispatches. FETCH_SIZE and
+pt_render_kernel; product build INSTR=0) counters averaged over its dispatches,
+times the dispatches per render of a multi-pass launch (roofline.passes). FETCH_SIZE and
 WRITE_SIZE are in KiB. gfx950 correction (MI355X_MICROARCH.md, HBM section):
 FETCH_SIZE counts half the bytes of wide coalesced streaming reads, so the
 corrected read bytes are 2x FETCH_SIZE; WRITE_SIZE is exact for 16-B-per-lane
@@ -43,11 +44,14 @@ for n, args in enumerate(cfgs, 1):
     log = (root / f"c{n}_FETCH_SIZE.log").read_text()
     line = json.loads([x for x in log.splitlines() if x.startswith("{")][-1])
     cfg = line["config"]
-    key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_spp{cfg['spp']}_d{cfg['depth']}_{cfg['precision']}_n{line['n_gpus']}"
+    key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_spp{cfg['spp']}_d{cfg['depth']}_{cfg['precision']}_n{line['n_gpus']}{'_adaptive' if cfg.get('adaptive') else ''}"
     dom = next((k for k in ("pt_pool_kernel", "pt_chunk_kernel") if k in fetch), "pt_render_kernel")
-    f_kib, w_kib = fetch.get(dom, 0.0), write.get(dom, 0.0)
+    # per RENDER (the bench line's roofline divides by the whole launch's kernel time):
+    # a multi-pass launch makes `passes` dispatches of the path kernel per render
+    passes = int(line.get("roofline", {}).get("passes") or 1)
+    f_kib, w_kib = fetch.get(dom, 0.0) * passes, write.get(dom, 0.0) * passes
     entry = {
-        "kernel": dom,
+        "kernel": dom, "passes": passes,
         "fetch_size_kib": f_kib, "write_size_kib": w_kib,
         "hbm_bytes_per_launch": (2.0 * f_kib + w_kib) * 1024.0,
         "hbm_bytes_per_launch_raw": (f_kib + w_kib) * 1024.0,

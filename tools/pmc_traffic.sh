@@ -10,7 +10,7 @@ n=0
 for args in "$@"; do
   n=$((n+1))
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -d $R/gpurun_out/traffic/c${n}_$c -o run --output-format csv -- python3 $R/bench.py $args --steps 2 --warmup 0 --no-cpu --no-count > $R/gpurun_out/traffic/c${n}_$c.log 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -d $R/gpurun_out/traffic/c${n}_$c -o run --output-format csv -- python3 $R/bench.py $args --steps 2 --warmup 0 --no-cpu --no-count --no-parity > $R/gpurun_out/traffic/c${n}_$c.log 2>&1
     rc=$?; echo "cfg $n ($args) $c rc=$rc" >> $R/gpurun_out/traffic/summary.txt
     [ $rc -ge 124 ] && exit $rc
   done

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Fold the VALU counter passes (tools/pmc_valu.sh) into profiles/pmc_valu.json.
 
-Per configuration, for the dominant product kernel (pt_chunk_kernel, else
-pt_render_kernel; INSTR=0 build), counters averaged over its dispatches and
-the dispatch duration from the same runs' kernel traces. Derived figures
+Per configuration, for the dominant product kernel (pt_pool_kernel, else
+pt_chunk_kernel, else pt_render_kernel; INSTR=0 build), counters averaged over
+its dispatches and the dispatch duration from the same runs' kernel traces.
+Per-sample figures are per RENDER: a multi-pass launch (record budget) makes
+`passes` dispatches per render (the bench line's roofline.passes), so the
+per-dispatch average is multiplied by passes before dividing by the samples. Derived figures
 (units per MI355X_MICROARCH.md: SQ_ACTIVE_INST_* count quad-cycles,
 GRBM_GUI_ACTIVE is summed over the 8 XCDs):
   clock_ghz   = GRBM_GUI_ACTIVE / 8 / duration
@@ -95,13 +98,17 @@ for n, args in enumerate(cfgs, 1):
     f64_flops = (c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + 2 * c["SQ_INSTS_VALU_FMA_F64"]) * 64 * lane
     f32_flops = (c["SQ_INSTS_VALU_ADD_F32"] + c["SQ_INSTS_VALU_MUL_F32"] + 2 * c["SQ_INSTS_VALU_FMA_F32"]) * 64 * lane
     cfg = line["config"]
-    key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_spp{cfg['spp']}_d{cfg['depth']}_{cfg['precision']}_n{line['n_gpus']}{TAG}"
-    samples = cfg["width"] * cfg["height"] * cfg["spp"]
+    # a render of a multi-pass launch (config 4's rain, config 5) is `passes` dispatches:
+    # counters are averaged per dispatch above, so per-sample figures scale by passes
+    passes = int(line.get("roofline", {}).get("passes") or 1)
+    key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_spp{cfg['spp']}_d{cfg['depth']}_{cfg['precision']}_n{line['n_gpus']}{'_adaptive' if cfg.get('adaptive') else ''}{TAG}"
+    samples = cfg.get("samples_per_frame") or cfg["width"] * cfg["height"] * cfg["spp"]
     entry = {
         "kernel": kern, "duration_ms": round(dur * 1e3, 4), "clock_ghz": round(clock / 1e9, 3),
         "valu_busy": round(busy, 4), "lane_util": round(lane, 4),
-        "valu_insts_per_sample": round(c["SQ_INSTS_VALU"] * 64 / samples, 1),
-        "salu_insts_per_sample": round(c["SQ_INSTS_SALU"] * 64 / samples, 1),
+        "passes": passes, "launch_ms": round(dur * passes * 1e3, 4),
+        "valu_insts_per_sample": round(c["SQ_INSTS_VALU"] * passes * 64 / samples, 1),
+        "salu_insts_per_sample": round(c["SQ_INSTS_SALU"] * passes * 64 / samples, 1),
         "f64_tflops": round(f64_flops / dur / 1e12, 3), "f64_peak_tflops": F64_PEAK,
         "f64_frac": round(f64_flops / dur / 1e12 / F64_PEAK, 4),
         "f32_tflops": round(f32_flops / dur / 1e12, 3), "f32_peak_tflops": F32_PEAK,

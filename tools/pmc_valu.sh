@@ -13,7 +13,7 @@ for args in "$@"; do
   while read -r line; do
     [ -z "$line" ] && continue
     i=$((i+1))
-    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $line -d $R/$V/c${n}_p$i -o run --output-format csv -- python3 $R/bench.py $args --steps 2 --warmup 0 --no-cpu --no-count > $R/$V/c${n}_p$i.log 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $line -d $R/$V/c${n}_p$i -o run --output-format csv -- python3 $R/bench.py $args --steps 2 --warmup 0 --no-cpu --no-count --no-parity > $R/$V/c${n}_p$i.log 2>&1
     rc=$?; echo "cfg $n ($args) pass $i rc=$rc" >> $R/$V/summary.txt
     [ $rc -ge 124 ] && exit $rc
   done < $R/tools/pmc_passes_valu.txt
