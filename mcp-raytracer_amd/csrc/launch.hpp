@@ -48,6 +48,9 @@ hipError_t launch_render_fp32(const KernelVariant& v, const DevScene& S, const R
 // Per-pixel in-order sum of a chunked pass's sample buffer + outputs + stats.
 hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
                         const SampleBuf& sb, hipStream_t stream);
+// One adaptive-sampling round's accumulate / convergence pass over the pass's slots.
+hipError_t launch_adapt(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
+                        const SampleBuf& sb, const AdaptRound& ar, hipStream_t stream);
 // Resets the stats words / counters / tile counter before a render.
 hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* counters, unsigned int* tile_counter,
                              hipStream_t stream);

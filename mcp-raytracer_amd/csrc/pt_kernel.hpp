@@ -2133,8 +2133,27 @@ struct SampleBuf {
     int32_t n_items;
     int32_t refill_min;  // idle lanes that trigger a hand-out (all-idle always does)
     int32_t min_ready;   // resumable fast traversal: lanes done walking before the wave shades
+    // Adaptive-sampling rounds (pt_adapt_kernel): the pass's record slot a renders the launch
+    // slot act[a] (tile * 64 + lane over the launch's tiles; tile0 is 0), samples s_base + s.
+    // act == nullptr: slot a is pass tile tile0 + a / 64, lane a % 64, samples from 0.
+    const int32_t* act;
+    int32_t s_base;
     int32_t s0[kMaxPhases], chunk[kMaxPhases], nch[kMaxPhases], item_base[kMaxPhases];
     double rnch[kMaxPhases];  // 1.0 / nch
+};
+
+// Adaptive sampling in rounds (pt_adapt_kernel): a pixel's running PixelStats
+// between rounds (src/render-utils/renderStats.ts:66-88), by launch slot.
+struct AdaptPix {
+    float4 c;     // colour sum (fp32, sample order), n (int bits)
+    double2 ill;  // sumIll, sumIll2
+    int4 b;       // bounce sum (low 32 bits), min, max, bounce sum (high 32 bits)
+};
+struct AdaptRound {
+    AdaptPix* state;        // launch slots (tile * 64 + lane)
+    int32_t* next_act;      // the pixels still sampling after this round
+    unsigned int* next_count;
+    int32_t len;            // samples of this round
 };
 
 #ifndef RT_REC_NT
@@ -2177,6 +2196,19 @@ __device__ __forceinline__ void item_pixel(const RtRegion& reg, int tiles_x, dou
     const int ty = udiv(gt, tiles_x, rtx);
     i = reg.x + (gt - ty * tiles_x) * kTile + (l & (kTile - 1));
     j = reg.y + ty * kTile + (l / kTile);
+}
+// Record slot a of the pass -> its pixel (i, j) (through the adaptive round's
+// active list when there is one); false past the pass's slots or outside the region.
+template <class SB>
+__device__ __forceinline__ bool slot_pixel(const SB& sb, const RtRegion& reg, int tiles_x, double rtx, int endX,
+                                           int endY, int a, int& i, int& j) {
+    int ls = a;
+    if (sb.act) {
+        if (a >= sb.slots) return false;
+        ls = sb.act[a];
+    }
+    item_pixel(reg, tiles_x, rtx, sb.tile0 + (ls >> 6), ls & 63, i, j);
+    return i < endX && j < endY;
 }
 
 // The guided schedule's phase rows, copied to LDS at kernel start: an item's
@@ -2296,8 +2328,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 if (slot < 0 && rank < take) {
                     int tl, l, s1, e1;
                     item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
-                    item_pixel(reg, tiles_x, rtx, sb.tile0 + tl, l, i, j);
-                    if (i < endX && j < endY) {
+                    if (slot_pixel(sb, reg, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
                         slot = tl * 64 + l;
                         s = s1;
                         s_end = e1;
@@ -2332,7 +2363,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             // cut-off / roulette, and the walk of its ray
             if (slot >= 0 && !walking) {
                 if (new_path) {
-                    path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)s);
+                    path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(sb.s_base + s));
                     new_path = false;
                 }
                 V3 c;
@@ -2356,7 +2387,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             const RtCamera& C = cam_opaque();
             prof_trip<PROF>(pf);
             if (new_path) {
-                path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)s);
+                path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(sb.s_base + s));
                 new_path = false;
                 psec<PROF>(pf, PR_NEWPATH);
             }
@@ -2636,8 +2667,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                     if (k >= 0 && phase == PH_ITEM && rank < take) {
                         int tl, l, s1, e1, i, j;
                         item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
-                        item_pixel(reg, tiles_x, rtx, sb.tile0 + tl, l, i, j);
-                        if (i < endX && j < endY) {
+                        if (slot_pixel(sb, reg, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
                             slot = tl * 64 + l;
                             s = s1;
                             clog2 = __builtin_ctz((uint32_t)(e1 - s1));  // power-of-two, aligned chunks
@@ -2653,10 +2683,10 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 const RtCamera& C = cam_opaque();
                 Path<false> P;
                 if (phase == PH_NEW) {
-                    int i, j;  // the slot's pixel (the hand-out's item_pixel)
-                    item_pixel(reg, tiles_x, rtx, sb.tile0 + (slot >> 6), slot & 63, i, j);
+                    int i, j;  // the slot's pixel (the hand-out's slot_pixel)
+                    slot_pixel(sb, reg, tiles_x, rtx, endX, endY, slot, i, j);
                     path_begin<Real, false>(C, P, pixel_center<Real>(C, i, j),
-                                            (uint32_t)j * (uint32_t)C.width + (uint32_t)i, (uint32_t)s);
+                                            (uint32_t)j * (uint32_t)C.width + (uint32_t)i, (uint32_t)(sb.s_base + s));
                 } else {
                     P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
                     P.o = V3{g1.x, g1.y, g1.z};

@@ -135,6 +135,126 @@ __global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegi
     }
 }
 
+// One round of adaptive sampling (src/camera.ts:400-425, pixelConverged 348-368):
+// every pixel of the round's active list adds the round's samples to its running
+// PixelStats in sample order, checking convergence after each one exactly as the
+// reference's while loop does (pixel_converged tests n % aBatch itself), and stops
+// at the first converged check - samples the round rendered past it are dropped,
+// so the result is the sequential loop's. Finished pixels (converged or n ==
+// samples) get finalColor / u8 / RenderStats; the rest carry their state to the
+// next round's active list (order irrelevant: every pixel's result depends on its
+// own samples only). One atomic per block-iteration appends to the list.
+__global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
+                                                              SampleBuf sb, AdaptRound ar) {
+    const RtCamera& C = S0.cam;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    const double rtx = 1.0 / (double)tiles_x;
+    const int endX = min(reg.x + reg.width, C.width), endY = min(reg.y + reg.height, C.height);
+    PixStats st;
+    __shared__ unsigned int wcnt[kAccBlock / kWave];
+    __shared__ unsigned int wbase;
+    const int stride = gridDim.x * blockDim.x;
+    const int n_iter = (sb.slots + stride - 1) / stride;  // block-uniform trip count (the append syncs)
+    for (int it = 0; it < n_iter; ++it) {
+        const int a = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        int i = 0, j = 0;
+        const bool valid = a < sb.slots && slot_pixel(sb, reg, tiles_x, rtx, endX, endY, a, i, j);
+        const int ls = valid ? (sb.act ? sb.act[a] : sb.tile0 * kWave + a) : 0;
+        bool carry = false;
+        if (valid) {
+            V3 color = v3(0, 0, 0);
+            int n = 0, bmin = 0x7fffffff, bmax = 0;
+            unsigned long long bsum = 0;
+            double sIll = 0.0, sIll2 = 0.0;
+            if (sb.s_base > 0) {
+                const AdaptPix q = ar.state[ls];
+                color = v3(q.c.x, q.c.y, q.c.z);
+                n = __float_as_int(q.c.w);
+                sIll = q.ill.x;
+                sIll2 = q.ill.y;
+                bsum = (unsigned long long)(uint32_t)q.b.x | ((unsigned long long)(uint32_t)q.b.w << 32);
+                bmin = q.b.y;
+                bmax = q.b.z;
+            }
+            bool done = false;
+            const float4* rec = sb.rec + (size_t)a * sb.stride_slot;
+            for (int k = 0; k < ar.len && !done; ++k) {
+                // PixelStats.add (renderStats.ts:76-88), then the while condition
+                const float4 r = rec[(size_t)k * sb.stride_s];
+                const V3 c = v3(r.x, r.y, r.z);
+                color = add(color, c);
+                ++n;
+                const int b = __float_as_int(r.w);
+                bsum += (unsigned long long)b;
+                bmin = min(bmin, b);
+                bmax = max(bmax, b);
+                const double il = illuminance(c);
+                sIll += il;
+                sIll2 += il * il;
+                done = n >= C.n_samples || pixel_converged(C, n, sIll, sIll2);
+            }
+            if (done) {
+                const uint32_t opix = out.packed ? (uint32_t)ls : (uint32_t)j * (uint32_t)C.width + (uint32_t)i;
+                finish_pixel(C, out, opix, color, n, bsum, bmin, bmax, st);
+            } else {
+                AdaptPix q;
+                q.c = make_float4(color.x, color.y, color.z, __int_as_float(n));
+                q.ill = make_double2(sIll, sIll2);
+                q.b = make_int4((int)(uint32_t)bsum, bmin, bmax, (int)(uint32_t)(bsum >> 32));
+                ar.state[ls] = q;
+                carry = true;
+            }
+        }
+        // append the carried pixels: one atomic per block and iteration
+        const unsigned long long m = __ballot(carry);
+        if (lane == 0) wcnt[w] = (unsigned int)__popcll(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned int tot = 0;
+            for (int q = 0; q < kAccBlock / kWave; ++q) {
+                const unsigned int c = wcnt[q];
+                wcnt[q] = tot;
+                tot += c;
+            }
+            wbase = tot ? atomicAdd(ar.next_count, tot) : 0u;
+        }
+        __syncthreads();
+        if (carry) {
+            const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            ar.next_act[wbase + wcnt[w] + (unsigned int)r] = ls;
+        }
+        __syncthreads();
+    }
+    __shared__ unsigned long long red[kAccBlock / kWave][7];
+    const unsigned long long v[7] = {wave_sum(st.pixels), wave_sum(st.samples), wave_min(st.smin), wave_max(st.smax),
+                                     wave_sum(st.b),      wave_min(st.bmin),    wave_max(st.bmax)};
+    if (lane == 0)
+        for (int q = 0; q < 7; ++q) red[w][q] = v[q];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t[7];
+        for (int q = 0; q < 7; ++q) t[q] = red[0][q];
+        for (int u = 1; u < kAccBlock / kWave; ++u) {
+            t[0] += red[u][0];
+            t[1] += red[u][1];
+            t[2] = min(t[2], red[u][2]);
+            t[3] = max(t[3], red[u][3]);
+            t[4] += red[u][4];
+            t[5] = min(t[5], red[u][5]);
+            t[6] = max(t[6], red[u][6]);
+        }
+        stats_atomics(out, t[0], t[1], t[2], t[3], t[4], t[5], t[6], 0ull);
+    }
+}
+
+hipError_t launch_adapt(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
+                        const SampleBuf& sb, const AdaptRound& ar, hipStream_t stream) {
+    const int grid = std::max(1, std::min((sb.slots + kAccBlock - 1) / kAccBlock, 2 * 256 * 1024 / kAccBlock));
+    hipLaunchKernelGGL(pt_adapt_kernel, dim3(grid), dim3(kAccBlock), 0, stream, S, reg, out, tiles_x, sb, ar);
+    return hipGetLastError();
+}
+
 hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
                         const SampleBuf& sb, hipStream_t stream) {
     // about two blocks' worth of slots per thread-slot of the chip: 2 x 256 CUs x 1024 threads

@@ -149,6 +149,11 @@ struct rt_camera {
         d_rad = nullptr;
         d_sbuf = nullptr;
         sbuf_cap = 0;
+        free_adapt_buffers();
+        if (d_acount) (void)hipFree(d_acount);
+        d_acount = nullptr;
+        if (h_acount) (void)hipHostFree(h_acount);
+        h_acount = nullptr;
         for (hipEvent_t& e : ev)
             if (e) (void)hipEventDestroy(e), e = nullptr;
         ev.clear();
@@ -339,7 +344,10 @@ struct rt_camera {
         // resident wave; with the hand-out rules above the chunked kernel is faster there
         // too (rain-50 1080p spp512: 50.7 -> 44.1 ms, profiles/r02/sched/), records and all.
         const bool chunked = env_flag("RT_AMD_CHUNKED", true);
-        if (C.adaptive || C.n_samples <= 0 || !chunked) {
+        // Adaptive sampling runs in rounds on the chunked / pool kernels (pt_adapt_kernel
+        // settles each round in sample order); RT_AMD_ADAPT_ROUNDS=0 keeps the sequential kernel.
+        const bool rounds = C.adaptive && env_flag("RT_AMD_ADAPT_ROUNDS", true);
+        if (C.n_samples <= 0 || !chunked || (C.adaptive && !rounds)) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
             hip_check(hipEventRecord(pass_event(0, 0), stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, g, nullptr, stream)
@@ -351,12 +359,7 @@ struct rt_camera {
             last_kernel = RT_KERNEL_SEQUENTIAL;
             return;
         }
-        // chunked kernel: passes over at most sbuf_budget bytes of per-sample records
-        const size_t rec_per_tile = (size_t)kWave * (size_t)C.n_samples * sizeof(float4);
-        const long pass_tiles = std::max<long>(1, std::min<long>(mine, (long)(sbuf_budget() / rec_per_tile)));
-        ensure_sbuf((size_t)pass_tiles * rec_per_tile);
         SampleBuf sb{};
-        sb.rec = d_sbuf;
 
         // Stage-compacted pool kernel (pt_pool_kernel): possible for product brute-force
         // launches without an emission stack whose per-wave path pools fit in LDS beside
@@ -364,20 +367,21 @@ struct rt_camera {
         // split by branch (Cornell 800^2 spp256 ref 16.82 ms vs chunked ~18.9 ms; fp32
         // 14.12 vs 14.23 ms, profiles/r02/asplit/). RT_AMD_POOL_KERNEL=0/1 overrides.
         S.lds_pool_off = (int32_t)((g.lds_bytes + 15) / 16 * 16);
-        v.pool = !v.emit && (count == 0 || (RT_POOL_PROF && count == 2 && prec == PREC_REF)) && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
+        const bool pool_ok = !v.emit && (count == 0 || (RT_POOL_PROF && count == 2 && prec == PREC_REF)) && v.trav == TRAV_BRUTE && C.width < 65536 && C.height < 65536 &&
                  C.n_samples <= 65535 && C.depth <= 250 && build.mats.size() < (1u << 21) &&  // 56-byte slot fields
                  build.prims.size() < (1u << 14) &&
                  (size_t)S.lds_pool_off + pool_lds_bytes() + static_lds_bytes(count, true) <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
-        // guided schedule: half of the remaining samples per phase, chunks halving.
-        // First-phase chunk from the samples per resident lane: an item is the
-        // critical path of its pixel, so small per-launch workloads (a rank's
-        // share of the image, small images) or a few very expensive pixels (rays
-        // grazing a field of spheres) need short items, while large ones amortise
-        // the hand-out over long items (tools/tail_probe.py sweep).
-        {
+        // guided schedule of `nsamp` samples over `slots` pixel slots: half of the remaining
+        // samples per phase, chunks halving. First-phase chunk from the samples per resident
+        // lane: an item is the critical path of its pixel, so small per-launch workloads (a
+        // rank's share of the image, small images) or a few very expensive pixels (rays
+        // grazing a field of spheres) need short items, while large ones amortise the
+        // hand-out over long items (tools/tail_probe.py sweep).
+        auto schedule = [&](double slots, int nsamp) {
+            v.pool = pool_ok;
             // spl: samples per resident lane of this launch.
-            const double spl = (double)mine * kWave * (double)C.n_samples / ((double)cus * kBlockChunk);
+            const double spl = slots * (double)nsamp / ((double)cus * kBlockChunk);
             // Brute-force scenes in the chunked kernel: two tile-chunks per atomic from 512 spl
             // and first items of spl / 8 (round 1, profiles/r01/sweep_b/).
             // The pool kernel (96 path slots per wave, any slot takes any item) wants wider takes
@@ -407,15 +411,15 @@ struct rt_camera {
             // power-of-two chunks: items are aligned to their chunk (the pool kernel derives an
             // item's end from its sample index)
             auto pow2floor = [](int x) { int p = 1; while (p * 2 <= x) p *= 2; return p; };
-            int s0 = 0, c = pow2floor(std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, C.n_samples / 2))), np = 0;
+            int s0 = 0, c = pow2floor(std::min(env_int("RT_AMD_CHUNK", c_auto), std::max(1, nsamp / 2))), np = 0;
             if (!env_flag("RT_AMD_GUIDED", true)) {  // uniform chunks (A/B)
-                c = pow2floor(std::max(1, std::min(env_int("RT_AMD_CHUNK", c_auto), C.n_samples)));
-                const int full = C.n_samples / c;
+                c = pow2floor(std::max(1, std::min(env_int("RT_AMD_CHUNK", c_auto), nsamp)));
+                const int full = nsamp / c;
                 sb.s0[np] = 0; sb.chunk[np] = c; sb.nch[np] = full; ++np;
                 s0 = full * c;
             }
-            while (s0 < C.n_samples) {
-                const int rem = C.n_samples - s0;
+            while (s0 < nsamp) {
+                const int rem = nsamp - s0;
                 if (c <= 1 || np == kMaxPhases - 1) {  // final phase: 1-sample items
                     sb.s0[np] = s0; sb.chunk[np] = 1; sb.nch[np] = rem;
                     ++np;
@@ -439,24 +443,14 @@ struct rt_camera {
                 if (sb.s0[p] != covered) throw std::runtime_error("guided schedule: gap");
                 covered += sb.chunk[p] * sb.nch[p];
             }
-            if (covered != C.n_samples) throw std::runtime_error("guided schedule: coverage");
+            if (covered != nsamp) throw std::runtime_error("guided schedule: coverage");
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
-        }
+        };
+        // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
-        for (long t0 = 0; t0 < mine; t0 += pass_tiles, ++pass) {
-            const long nt = std::min(pass_tiles, mine - t0);
-            sb.tile0 = (int32_t)t0;
-            sb.slots = (int32_t)(nt * kWave);
-            // record layout: sample-major (default) or slot-major (RT_AMD_REC_SLOT_MAJOR=1, A/B)
-            if (env_flag("RT_AMD_REC_SLOT_MAJOR", false)) {
-                sb.stride_s = 1;
-                sb.stride_slot = C.n_samples;
-            } else {
-                sb.stride_s = sb.slots;
-                sb.stride_slot = 1;
-            }
+        auto run_pass = [&](bool first) {
             long items = 0;
             for (int p = 0; p < sb.n_phases; ++p) {
                 sb.item_base[p] = (int32_t)items;
@@ -464,7 +458,7 @@ struct rt_camera {
             }
             if (items >= (1l << 31) - (1l << 22)) throw std::runtime_error("chunked pass too large");  // counter headroom: 2 x grid waves x pool
             sb.n_items = (int32_t)items;
-            if (t0 > 0) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
+            if (!first) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = g;
             gp.grid = (int)std::max<long>(1, std::min<long>(items / (v.pool ? kBlockPool : kBlockChunk) + 1, (long)cus));
             if (v.pool) gp.lds_bytes = (size_t)S.lds_pool_off + pool_lds_bytes();
@@ -474,12 +468,114 @@ struct rt_camera {
                                              : launch_render_ref(v, S, reg, out, gp, &sb, stream);
             hip_check(e, "pt_chunk_kernel launch");
             hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
-            hip_check(launch_accum(S, reg, out, g.tiles_x, sb, stream), "pt_accum_kernel launch");
-            hip_check(hipEventRecord(pass_event(pass, 2), stream), "hipEventRecord");
+        };
+        if (rounds) {
+            launch_adaptive_rounds(S, reg, out, g, mine, sb, schedule, run_pass, pass, stream);
+        } else {
+            // fixed spp: passes over at most sbuf_budget bytes of per-sample records
+            const size_t rec_per_tile = (size_t)kWave * (size_t)C.n_samples * sizeof(float4);
+            const long pass_tiles = std::max<long>(1, std::min<long>(mine, (long)(sbuf_budget() / rec_per_tile)));
+            ensure_sbuf((size_t)pass_tiles * rec_per_tile);
+            sb.rec = d_sbuf;
+            schedule((double)mine * kWave, C.n_samples);
+            for (long t0 = 0; t0 < mine; t0 += pass_tiles, ++pass) {
+                const long nt = std::min(pass_tiles, mine - t0);
+                sb.tile0 = (int32_t)t0;
+                sb.slots = (int32_t)(nt * kWave);
+                // record layout: sample-major (default) or slot-major (RT_AMD_REC_SLOT_MAJOR=1, A/B)
+                if (env_flag("RT_AMD_REC_SLOT_MAJOR", false)) {
+                    sb.stride_s = 1;
+                    sb.stride_slot = C.n_samples;
+                } else {
+                    sb.stride_s = sb.slots;
+                    sb.stride_slot = 1;
+                }
+                run_pass(t0 == 0);
+                hip_check(launch_accum(S, reg, out, g.tiles_x, sb, stream), "pt_accum_kernel launch");
+                hip_check(hipEventRecord(pass_event(pass, 2), stream), "hipEventRecord");
+            }
         }
         n_passes = pass;
         ev_accum = true;
         last_kernel = v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
+    }
+
+    // Adaptive sampling in rounds (src/camera.ts:400-425). Round r renders samples
+    // [s_base, s_base + len) of every pixel still sampling - speculatively, since a pixel
+    // may converge inside the round - on the chunked / pool kernels; pt_adapt_kernel then
+    // adds them to each pixel's running PixelStats in sample order with the reference's
+    // convergence check after every sample, finishes converged / complete pixels and
+    // compacts the rest into the next round's active list. Rounds double in length from
+    // two convergence batches (aBatch) so a pixel renders at most one round past its
+    // convergence; the pixel count of each round comes back to the host (one small copy).
+    template <class Sched, class Pass>
+    void launch_adaptive_rounds(DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g, long mine,
+                                SampleBuf& sb, Sched& schedule, Pass& run_pass, int& pass, hipStream_t stream) {
+        const RtCamera& C = build.cam;
+        const long slots_all = mine * kWave;
+        ensure_adapt((size_t)slots_all);
+        const double ab = C.a_batch;
+        const int batch = (ab >= 1.0 && ab < 65536.0) ? (int)ab : std::max(1, std::min(C.n_samples, 16));
+        int len = batch * std::max(2, (env_int("RT_AMD_ADAPT_FIRST", 16) + batch - 1) / batch);
+        long n_act = slots_all;
+        const int32_t* act = nullptr;  // round 0: every slot of the launch (invalid pixels skipped)
+        int cur = 0;
+        AdaptRound ar{};
+        ar.state = d_astate;
+        ar.next_count = d_acount;
+        sb.stride_slot = 1;
+        for (int s_base = 0; n_act > 0 && s_base < C.n_samples; s_base += len, len *= 2) {
+            len = std::min(len, C.n_samples - s_base);
+            ar.len = len;
+            ar.next_act = d_act[1 - cur];
+            sb.s_base = s_base;
+            schedule((double)n_act, len);
+            const size_t rec_per_slot = (size_t)len * sizeof(float4);
+            const long pass_slots = std::max<long>(kWave, std::min<long>((n_act + kWave - 1) / kWave * kWave,
+                                                                        (long)(sbuf_budget() / rec_per_slot) / kWave * kWave));
+            ensure_sbuf((size_t)pass_slots * rec_per_slot);
+            sb.rec = d_sbuf;
+            hip_check(hipMemsetAsync(d_acount, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
+            for (long a0 = 0; a0 < n_act; a0 += pass_slots, ++pass) {
+                sb.slots = (int32_t)std::min<long>(pass_slots, n_act - a0);
+                sb.stride_s = sb.slots;
+                sb.act = act ? act + a0 : nullptr;
+                sb.tile0 = act ? 0 : (int32_t)(a0 / kWave);
+                run_pass(pass == 0);
+                hip_check(launch_adapt(S, reg, out, g.tiles_x, sb, ar, stream), "pt_adapt_kernel launch");
+                hip_check(hipEventRecord(pass_event(pass, 2), stream), "hipEventRecord");
+            }
+            hip_check(hipMemcpyAsync(h_acount, d_acount, sizeof(unsigned int), hipMemcpyDeviceToHost, stream),
+                      "hipMemcpyAsync");
+            hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+            n_act = (long)*h_acount;
+            act = d_act[1 - cur];
+            cur = 1 - cur;
+        }
+    }
+
+    // Adaptive rounds: per-slot running PixelStats, two active lists, the list counter.
+    AdaptPix* d_astate = nullptr;
+    int32_t* d_act[2] = {nullptr, nullptr};
+    unsigned int* d_acount = nullptr;
+    unsigned int* h_acount = nullptr;
+    size_t adapt_cap = 0;
+    void ensure_adapt(size_t slots) {
+        if (!h_acount) hip_check(hipHostMalloc((void**)&h_acount, sizeof(unsigned int), 0), "hipHostMalloc");
+        if (!d_acount) hip_check(hipMalloc(&d_acount, sizeof(unsigned int)), "hipMalloc");
+        if (slots <= adapt_cap) return;
+        free_adapt_buffers();
+        hip_check(hipMalloc(&d_astate, slots * sizeof(AdaptPix)), "hipMalloc(adaptive state)");
+        hip_check(hipMalloc(&d_act[0], slots * sizeof(int32_t)), "hipMalloc(active list)");
+        hip_check(hipMalloc(&d_act[1], slots * sizeof(int32_t)), "hipMalloc(active list)");
+        adapt_cap = slots;
+    }
+    void free_adapt_buffers() {
+        for (void* p : {(void*)d_astate, (void*)d_act[0], (void*)d_act[1]})
+            if (p) (void)hipFree(p);
+        d_astate = nullptr;
+        d_act[0] = d_act[1] = nullptr;
+        adapt_cap = 0;
     }
 
     // Per-sample record buffer of the chunked kernel (grown on demand, kept).

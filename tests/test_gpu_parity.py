@@ -699,8 +699,10 @@ PACKED_CASES = {
              "chunked"),
     # the pool kernel's packed-index path
     "cornell_pool": ({"type": "cornell"}, {"width": 72, "samples": 8, "depth": 8, **NOADAPT}, {}, "pool"),
-    # adaptive sampling: the sequential kernel's packed index (tile * 64 + lane)
-    "adaptive": ({"type": "cornell"}, {"width": 72, "samples": 30, "depth": 8}, {}, "sequential"),
+    # adaptive sampling: the rounds' packed index (launch slot) and the sequential kernel's
+    "adaptive": ({"type": "cornell"}, {"width": 72, "samples": 30, "depth": 8}, {}, "pool"),
+    "adaptive_seq": ({"type": "cornell"}, {"width": 72, "samples": 30, "depth": 8}, {"RT_AMD_ADAPT_ROUNDS": "0"},
+                     "sequential"),
     # a record budget that forces several passes (the pass's tile offset in the packed index)
     "multipass": ({"type": "rain", "options": {"seed": 42}}, {"width": 72, "samples": 64, "depth": 8, **NOADAPT},
                   {"RT_AMD_SBUF_MB": "1"}, "chunked"),
@@ -773,3 +775,99 @@ def test_bench_two_ranks_one_gpu_assemble_the_frame(gpu):
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     print({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "frame_check")})
     assert line["n_gpus"] == 2 and line["frame_check"] is True
+
+
+# ---------------------------------------------------------------------------
+# Adaptive sampling in rounds (rt_api.cpp launch_adaptive_rounds, pt_adapt_kernel):
+# the chunked / pool kernels render each round's samples speculatively, the adapt
+# pass settles them in sample order with the reference's convergence check after
+# every sample (src/camera.ts:348-368,400-425). Same pixels, same stats as the
+# sequential kernel and the oracle.
+# ---------------------------------------------------------------------------
+ADAPT_CASES = {
+    # (scene, render options, env, kernel that renders the rounds)
+    "cornell_pool": ({"type": "cornell"}, {"width": 48, "samples": 90, "depth": 8}, {}, "pool"),
+    "cornell_batch1": ({"type": "cornell"}, {"width": 40, "samples": 37, "depth": 8, "aBatch": 1}, {}, "pool"),
+    "cornell_batch2_5": ({"type": "cornell"}, {"width": 40, "samples": 41, "depth": 8, "aBatch": 2.5,
+                                               "aTolerance": 0.2}, {}, "pool"),
+    "cornell_multipass": ({"type": "cornell"}, {"width": 64, "samples": 70, "depth": 8},
+                          {"RT_AMD_SBUF_MB": "1"}, "pool"),
+    "cornell_chunked": ({"type": "cornell"}, {"width": 40, "samples": 60, "depth": 8},
+                        {"RT_AMD_POOL_KERNEL": "0"}, "chunked"),
+    "spheres_bvh": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                    {"width": 48, "aspect": 1, "samples": 50, "depth": 8, "aTolerance": 0.1}, {}, "chunked"),
+    "default_scene": ({"type": "default"}, {"width": 40, "samples": 30, "depth": 10, "aTolerance": 0.1}, {},
+                      "chunked"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(ADAPT_CASES))
+def test_adaptive_rounds_match_oracle_and_sequential(rt, oracle, gpu, case, monkeypatch):
+    cfg, ro, env, kernel = ADAPT_CASES[case]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sd = rt.generate_scene_data(cfg)
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == kernel
+    if case == "cornell_multipass":
+        assert cam.pass_count() > 4  # several rounds, several passes each
+    orc = oracle.render(sd, ro)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"adaptive rounds {case}")
+    assert_stats_identical(st, orc["stats"])
+    assert st.samples["min"] < ro["samples"]  # some pixels converged early
+    monkeypatch.setenv("RT_AMD_ADAPT_ROUNDS", "0")
+    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
+    assert cam2.last_kernel() == "sequential"
+    assert_identical(rad, rgb, rad2, rgb2, f"adaptive rounds == sequential {case}")
+    assert st.samples == st2.samples and st.bounces == st2.bounces
+
+
+@pytest.mark.parametrize("mode", ["bounces", "samples"])
+def test_adaptive_rounds_render_modes_and_tile_groups(rt, oracle, gpu, mode):
+    """The visualisation modes and a 3-way tile split (a rank's share) through the
+    adaptive rounds: the three shares reassemble the oracle's frame, and their
+    merged stats are the whole frame's."""
+    import torch
+    from raytracer_amd import distributed as rtd
+    sd = rt.generate_scene_data({"type": "cornell"})
+    ro = {"width": 40, "samples": 50, "depth": 8, "mode": mode}
+    orc = oracle.render(sd, ro)
+    cam = rt.create_camera_from_scene_data(sd, ro)
+    W, H = cam.image_width, cam.image_height
+    rgb = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    rad = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    words = torch.zeros((3, 8), dtype=torch.int64, device="cuda")
+    for g in range(3):
+        cam.render_device(rgb_ptr=rgb.data_ptr(), radiance_ptr=rad.data_ptr(), tile_group=g, tile_groups=3,
+                          synchronize=True)
+        assert cam.last_kernel() == "pool"
+        cam.stats_words(words[g].data_ptr())
+    torch.cuda.synchronize()
+    assert_identical(rad.cpu().numpy(), rgb.cpu().numpy(), orc["radiance"], orc["rgb"], f"adaptive {mode} 3 groups")
+    st = rtd.stats_from_words(rtd.merge_stats_words(words).tolist())
+    assert_stats_identical(st, orc["stats"])
+
+
+def test_adaptive_full_size_headline_rows_match_oracle(rt, oracle, gpu):
+    """Cornell 800x800 spp 256 depth 16 with the reference's adaptive defaults
+    (aTolerance 0.05, aBatch 10; src/camera.ts:77-78): the whole frame through
+    the rounds, oracle rows bit for bit, and the frame equals the sequential
+    kernel's."""
+    sd = rt.generate_scene_data({"type": "cornell"})
+    ro = {"width": 800, "samples": 256, "depth": 16}
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == "pool"
+    W, H = cam.image_width, cam.image_height
+    assert st.pixels == W * H and st.samples["min"] < 256 and st.samples["max"] == 256
+    for y in (0, 311, 400, 799):
+        orc = oracle.render(sd, ro, region=(0, y, W, 1), threads=8)
+        assert_identical(rad[y:y + 1], rgb[y:y + 1], orc["radiance"][y:y + 1], orc["rgb"][y:y + 1],
+                         f"adaptive cornell 800 row {y}")
+    import os
+    os.environ["RT_AMD_ADAPT_ROUNDS"] = "0"
+    try:
+        cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
+    finally:
+        del os.environ["RT_AMD_ADAPT_ROUNDS"]
+    assert_identical(rad, rgb, rad2, rgb2, "adaptive 800 rounds == sequential")
+    assert st.samples == st2.samples and st.bounces == st2.bounces
