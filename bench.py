@@ -342,6 +342,7 @@ def main(argv=None):
                           stream=sptr, packed=world > 1)
         kt.append(cam.kernel_times())
     passes = cam.pass_count()
+    a_rounds, a_rendered = cam.adaptive_info()
     kernel_ms = sum(a for a, _ in kt) / len(kt)
     accum_ms = sum(b for _, b in kt) / len(kt)
     kind = cam.last_kernel()  # the path kernel the library launched (rt_camera_last_kernel)
@@ -382,6 +383,10 @@ def main(argv=None):
         rl = roofline(key, rt.build_id(), my_samples, kernel_ms, counters, my_pixels)
         rl.update({"kernel": kernel_name, "accum_kernel_ms": round(accum_ms, 4), "passes": passes,
                    "count_subsample": sub})
+        if args.adaptive:
+            rl["adaptive_rounds"] = {"rounds": a_rounds, "samples_rendered": a_rendered,
+                                     "samples_kept": int(my_samples),
+                                     "speculation": round(a_rendered / max(my_samples, 1) - 1.0, 4)}
         cpu = None
         if world == 1 and not args.no_cpu:
             log("cpu baseline")

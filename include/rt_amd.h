@@ -185,6 +185,12 @@ int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms);
 #define RT_STATS_WORDS 8
 int rt_camera_stats_words(rt_camera* cam, uint64_t* dst, void* stream);
 
+/* Adaptive sampling of the most recent render: the rounds it ran on the chunked /
+ * pool kernels (0: not adaptive, or the sequential kernel) and the samples those
+ * rounds rendered - at least RenderStats.samples.total; the excess is the
+ * speculation past each pixel's convergence (src/camera.ts:400-425 loop). */
+int rt_camera_adaptive_info(rt_camera* cam, int32_t* rounds, uint64_t* samples_rendered);
+
 /* Number of chunked-kernel passes of the most recent render (0 before any; the
  * sequential kernel counts as one). Passes split the per-sample record buffer. */
 int rt_camera_pass_count(rt_camera* cam, int32_t* passes);

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -335,6 +336,8 @@ struct rt_camera {
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
         n_passes = 0;
         last_kernel = RT_KERNEL_NONE;
+        adapt_rounds = 0;
+        adapt_rendered = 0;
         if (mine == 0) return;
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
@@ -451,10 +454,14 @@ struct rt_camera {
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
         auto run_pass = [&](bool first) {
+            // items come in (tile, chunk) groups of 64 (item_decode): a pass of an adaptive round
+            // whose slot count is not a multiple of 64 still numbers whole groups (the slots past
+            // sb.slots are skipped by slot_pixel)
+            const long group_slots = ((long)sb.slots + kWave - 1) / kWave * kWave;
             long items = 0;
             for (int p = 0; p < sb.n_phases; ++p) {
                 sb.item_base[p] = (int32_t)items;
-                items += (long)sb.slots * sb.nch[p];
+                items += group_slots * sb.nch[p];
             }
             if (items >= (1l << 31) - (1l << 22)) throw std::runtime_error("chunked pass too large");  // counter headroom: 2 x grid waves x pool
             sb.n_items = (int32_t)items;
@@ -516,7 +523,16 @@ struct rt_camera {
         ensure_adapt((size_t)slots_all);
         const double ab = C.a_batch;
         const int batch = (ab >= 1.0 && ab < 65536.0) ? (int)ab : std::max(1, std::min(C.n_samples, 16));
-        int len = batch * std::max(2, (env_int("RT_AMD_ADAPT_FIRST", 16) + batch - 1) / batch);
+        // first round: one convergence batch, then rounds x3 (tools/adapt_sweep.py, 800^2 / 1080p,
+        // profiles/r03/adapt_sweep.log: first 10 / 20 / 40 samples x growth 2 / 3 - one batch
+        // wastes least on scenes whose sky converges at the first check (rain 2.59 vs 3.36 ms at
+        // 20, spheres-500 5.87 vs 6.00 ms); Cornell, whose pixels converge at 10 or run to 256,
+        // prefers few long rounds: 15.94 ms with growth 3 vs 16.35 with 2, 15.56 at first 40)
+        int len = batch * std::max(1, (env_int("RT_AMD_ADAPT_FIRST", batch) + batch - 1) / batch);
+        const int grow = env_int("RT_AMD_ADAPT_GROW", 3);
+        const bool trace = env_flag("RT_AMD_ADAPT_LOG", false);
+        adapt_rounds = 0;
+        adapt_rendered = 0;
         long n_act = slots_all;
         const int32_t* act = nullptr;  // round 0: every slot of the launch (invalid pixels skipped)
         int cur = 0;
@@ -524,8 +540,12 @@ struct rt_camera {
         ar.state = d_astate;
         ar.next_count = d_acount;
         sb.stride_slot = 1;
-        for (int s_base = 0; n_act > 0 && s_base < C.n_samples; s_base += len, len *= 2) {
+        for (int s_base = 0; n_act > 0 && s_base < C.n_samples; s_base += len, len *= grow) {
             len = std::min(len, C.n_samples - s_base);
+            ++adapt_rounds;
+            adapt_rendered += (unsigned long long)n_act * (unsigned long long)len;
+            if (trace) std::fprintf(stderr, "[rt adaptive] round %d: samples [%d, %d) of %ld pixels\n", adapt_rounds,
+                                    s_base, s_base + len, n_act);
             ar.len = len;
             ar.next_act = d_act[1 - cur];
             sb.s_base = s_base;
@@ -554,6 +574,8 @@ struct rt_camera {
         }
     }
 
+    int adapt_rounds = 0;                   // rounds of the last adaptive render
+    unsigned long long adapt_rendered = 0;  // samples its rounds rendered (>= the samples kept)
     // Adaptive rounds: per-slot running PixelStats, two active lists, the list counter.
     AdaptPix* d_astate = nullptr;
     int32_t* d_act[2] = {nullptr, nullptr};
@@ -924,6 +946,14 @@ int rt_camera_stats_words(rt_camera* cam, uint64_t* dst, void* stream) {
     } catch (const std::exception& e) {
         return set_error(RT_ERR_DEVICE, e.what());
     }
+}
+
+int rt_camera_adaptive_info(rt_camera* cam, int32_t* rounds, uint64_t* samples_rendered) {
+    if (!cam || !rounds || !samples_rendered) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    *rounds = cam->adapt_rounds;
+    *samples_rendered = cam->adapt_rendered;
+    return RT_OK;
 }
 
 int rt_camera_pass_count(rt_camera* cam, int32_t* passes) {

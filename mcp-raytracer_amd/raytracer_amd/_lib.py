@@ -87,6 +87,7 @@ _SIGS = {
     "rt_debug_math": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "rt_camera_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "rt_camera_adaptive_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]),
     "rt_camera_stats_words": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_camera_pass_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rt_camera_last_kernel": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),

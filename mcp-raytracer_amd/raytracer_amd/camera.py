@@ -196,6 +196,13 @@ class Camera:
         device address `dst_ptr` on `stream` (rt_camera_stats_words)."""
         _lib.check(self._lib.rt_camera_stats_words(self._h, C.c_void_p(dst_ptr), C.c_void_p(stream)))
 
+    def adaptive_info(self):
+        """(rounds, samples rendered) of the last render's adaptive rounds
+        (rt_camera_adaptive_info); (0, 0) when it was not adaptive or ran sequentially."""
+        r, n = C.c_int32(), C.c_uint64()
+        _lib.check(self._lib.rt_camera_adaptive_info(self._h, C.byref(r), C.byref(n)))
+        return int(r.value), int(n.value)
+
     def pass_count(self) -> int:
         """Chunked-kernel passes of the last render (rt_camera_pass_count)."""
         n = C.c_int32()
