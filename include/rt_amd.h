@@ -114,7 +114,9 @@ enum {
  * at [RT_CT_WORDS + RT_PR_WORDS + RT_PR_LOOP + k]. */
 enum {
     RT_PR_NEWPATH = 0, RT_PR_RR, RT_PR_HIT, RT_PR_MISS, RT_PR_HITREC, RT_PR_SCATTER, RT_PR_SAMPLE, RT_PR_PDF,
-    RT_PR_ACC, RT_PR_TILE, RT_PR_LOOP, RT_PR_TRIPS, RT_PR_WORDS
+    RT_PR_ACC, RT_PR_TILE,
+    RT_PR_NODE, RT_PR_LEAF,  /* lane counts only (no cycles): the resumable walk's node steps and leaf tests */
+    RT_PR_LOOP, RT_PR_TRIPS, RT_PR_WORDS
 };
 /* work_counters arrays passed to rt_camera_render_device hold this many entries. */
 #define RT_COUNTER_WORDS 64
@@ -197,10 +199,11 @@ int rt_camera_pass_count(rt_camera* cam, int32_t* passes);
 
 /* Path kernel of the most recent render: RT_KERNEL_NONE before any,
  * RT_KERNEL_SEQUENTIAL (wave per 8x8 tile, adaptive sampling), RT_KERNEL_CHUNKED
- * (lane work pool + in-order accumulate) or RT_KERNEL_POOL (stage-compacted
- * path pools + in-order accumulate). Diagnostics and tests; no reference
+ * (lane work pool + in-order accumulate), RT_KERNEL_POOL (stage-compacted
+ * path pools + in-order accumulate) or RT_KERNEL_WPOOL (walkers over LDS path
+ * slots, BVH scenes). Diagnostics and tests; no reference
  * counterpart (the reference has one CPU loop, src/camera.ts:388-431). */
-enum { RT_KERNEL_NONE = 0, RT_KERNEL_SEQUENTIAL = 1, RT_KERNEL_CHUNKED = 2, RT_KERNEL_POOL = 3 };
+enum { RT_KERNEL_NONE = 0, RT_KERNEL_SEQUENTIAL = 1, RT_KERNEL_CHUNKED = 2, RT_KERNEL_POOL = 3, RT_KERNEL_WPOOL = 4 };
 int rt_camera_last_kernel(rt_camera* cam, int32_t* kernel);
 
 /* Frees the camera's device resources (scene copy, frame and record buffers,

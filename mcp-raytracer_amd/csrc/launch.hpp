@@ -18,7 +18,8 @@ struct LaunchGeom {
     int my_tiles;
     int grid;
     size_t lds_bytes;  // traversal stack + the LDS-resident scene prefix
-    int lds_level;     // LDS-resident scene: 0 none, 1 traversal data + prims, 2 also mats + lights
+    int lds_level;     // LDS-resident scene: 0 none, 1 traversal data + prims, 2 also mats + lights,
+                       // 3 traversal data only (walker-pool kernel)
 };
 
 // LDS budget (stack + [tnodes][prims]) up to which the scene is copied into LDS.
@@ -38,6 +39,7 @@ struct KernelVariant {
     int trav;    // TRAV_FAST / TRAV_REFERENCE / TRAV_BRUTE (resolved, never AUTO)
     bool defer = false;  // TRAV_FAST: deferred exact sphere tests (TRAV_FAST_DEFER kernels)
     bool pool = false;   // chunked passes run the stage-compacted pool kernel (pt_pool_kernel)
+    bool wpool = false;  // chunked passes run the walker-pool kernel (pt_wpool_kernel, BVH scenes)
 };
 
 // sb == nullptr: the sequential-pixel kernel; else the chunked kernel over sb's pass.

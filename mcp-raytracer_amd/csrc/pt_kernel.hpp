@@ -59,6 +59,7 @@ struct DevScene {
     int32_t off_tsph;                   // byte offset of tsph in the blob
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
     int32_t lds_pool_off;               // pool kernel: byte offset of the per-wave path pools (after the scene)
+    int32_t wpool_k;                    // walker-pool kernel: path slots per wave (<= 255)
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
@@ -87,12 +88,16 @@ enum : unsigned long long { ERR_NO_BACKGROUND = 1ull, ERR_EMIT_STACK = 2ull };
 // Diagnostic build (INSTR == 2): wave-cycles spent in each section of the path
 // loop (s_memtime, summed over waves), stored after the CT_WORDS counters.
 enum {
-    PR_NEWPATH = 0, PR_RR, PR_HIT, PR_MISS, PR_HITREC, PR_SCATTER, PR_SAMPLE, PR_PDF, PR_ACC, PR_TILE, PR_LOOP,
-    PR_TRIPS, PR_WORDS
+    PR_NEWPATH = 0, PR_RR, PR_HIT, PR_MISS, PR_HITREC, PR_SCATTER, PR_SAMPLE, PR_PDF, PR_ACC, PR_TILE,
+    PR_NODE, PR_LEAF,  // lane counts only (no cycles): node-step and leaf-test iterations of the walk
+    PR_LOOP, PR_TRIPS, PR_WORDS
 };
 // INSTR == 2 also records, per section k < PR_LOOP, the lanes active when a wave
 // ended it (summed, at CT_WORDS + PR_WORDS + k) and how many times a wave did
 // (at CT_WORDS + PR_WORDS + PR_LOOP + k): active lanes per execution of a section.
+struct Prof;  // diagnostic section timer (below)
+template <bool PROF>
+__device__ __forceinline__ void pcount(Prof& pf, int k);
 constexpr int kCounterWords = 64;  // CT_WORDS + PR_WORDS + 2 * PR_LOOP, rounded up
 static_assert(CT_WORDS + PR_WORDS + 2 * PR_LOOP <= kCounterWords, "counter words");
 
@@ -981,9 +986,9 @@ __device__ __forceinline__ void fast_walk_begin(const DevScene& S, V3 o, V3 d, F
 // Called by the whole wave with uniform control flow; lanes with `walking`
 // advance their walks. Returns when no lane walks, or (unless `drain`) after at
 // least one round once `min_ready` lanes of the wave are not walking.
-template <class Real, bool COUNT, bool DEFER>
+template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride>
 __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, bool& walking,
-                                                 int* stk, int min_ready, bool drain, uint32_t* cnt) {
+                                                 int* stk, int min_ready, bool drain, uint32_t* cnt, Prof* pf = nullptr) {
     const FRay f = make_fray(o, d);
     const RayK<Real> r = make_ray<Real>(o, d);
     float* stkt = nullptr;
@@ -1000,7 +1005,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             auto pop = [&]() -> int {
                 if (sp > 0) {
                     --sp;
-                    return stk[sp * kStackStride];
+                    return stk[sp * STRIDE];
                 }
                 return kTravDone;
             };
@@ -1049,7 +1054,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
 #pragma unroll
                 for (int c = 3; c >= 1; --c) {
                     if (kr[c] != kTravDone) {
-                        stk[sp * kStackStride] = kr[c];
+                        stk[sp * STRIDE] = kr[c];
                         ++sp;
                     }
                 }
@@ -1064,7 +1069,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 const bool hb = slab(nd.box[1], f, thi, tb);
                 if (ha && hb) {
                     const bool a_first = ta <= tb;
-                    stk[sp * kStackStride] = a_first ? nd.box[1].a : nd.box[0].a;
+                    stk[sp * STRIDE] = a_first ? nd.box[1].a : nd.box[0].a;
                     ++sp;
                     return a_first ? nd.box[0].a : nd.box[1].a;
                 }
@@ -1075,6 +1080,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             // one round of closest_hit_fast's parked-leaf walk
             int ref = W.ref, leaf = W.leaf;
             while (ref >= 0) {
+                if (PROF) pcount<PROF>(*pf, PR_NODE);
                 ref = node_step(ref);
                 if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
                     leaf = ref;
@@ -1087,6 +1093,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 ref = pop();
             }
             while (leaf != kTravDone) {
+                if (PROF) pcount<PROF>(*pf, PR_LEAF);
                 leaf_test<Real, COUNT, DEFER>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
                 if (ref < 0 && ref != kTravDone) {
@@ -1641,6 +1648,18 @@ __device__ __forceinline__ void psec(Prof& pf, int k) {
         }
     }
 }
+// Lane count of one execution of section k, without charging cycles (loop bodies too
+// short for a timer: node steps, leaf tests).
+template <bool PROF>
+__device__ __forceinline__ void pcount(Prof& pf, int k) {
+    if (PROF) {
+        const unsigned long long m = __ballot(1);
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) {
+            pf.w[2 + PR_WORDS + k] += (unsigned long long)__popcll(m);
+            pf.w[2 + 2 * PR_WORDS + k] += 1ull;
+        }
+    }
+}
 template <bool PROF>
 __device__ __forceinline__ void prof_trip(Prof& pf) {
     if (PROF) {
@@ -1994,7 +2013,8 @@ __device__ __forceinline__ void publish_counters(const RenderOut& out, const uin
 // Workgroup prologue shared by the render kernels: LDS-resident scene data
 // (one cooperative copy per workgroup) and this thread's stack columns.
 // LDSS 0: all scene reads from global memory; 1: the traversal data and the
-// primitive records in LDS; 2: also the material and light tables. (Wave-
+// primitive records in LDS; 2: also the material and light tables; 3 (walker-pool
+// kernel): the traversal data only ([tnodes][tprims][tsph]), primitive records global. (Wave-
 // uniform reads - the brute-force primitive loop, the light list - stay on
 // scalar loads from the global copy.)
 template <int LDSS>
@@ -2008,8 +2028,8 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
         S.tsph = reinterpret_cast<const float4*>(b + S0.off_tsph);
-        S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
-        if (LDSS > 1) {
+        if (LDSS != 3) S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);  // 3: the walk's data only
+        if (LDSS == 2) {
             S.mats = reinterpret_cast<const RtMat*>(b + S0.off_mats);
             S.lights = reinterpret_cast<const RtLight*>(b + S0.off_lights);
             S.onbs = reinterpret_cast<const RtOnb*>(b + S0.off_onbs);
@@ -2302,7 +2322,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     Path<EMIT> P;
     const double rtx = 1.0 / (double)tiles_x;
     // resumable fast traversal (product builds): per-lane walk state across iterations
-    constexpr bool RS = RT_RESUME && trav_fast(TRAV) && INSTR == 0;
+    constexpr bool RS = RT_RESUME && trav_fast(TRAV) && INSTR != 1;  // (INSTR 2: timed sections)
     FastWalk<Real> W;
     bool walking = false;
 
@@ -2359,12 +2379,14 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 else slot = -1;
             };
             const RtCamera& C = cam_opaque();
+            prof_trip<PROF>(pf);
             // lanes between rays: start a path if needed, then the level's depth
             // cut-off / roulette, and the walk of its ray
             if (slot >= 0 && !walking) {
                 if (new_path) {
                     path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(sb.s_base + s));
                     new_path = false;
+                    psec<PROF>(pf, PR_NEWPATH);
                 }
                 V3 c;
                 if (path_pre<Real, EMIT, PROF>(C, P, pf, c)) {
@@ -2374,15 +2396,18 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                     walking = true;
                 }
             }
+            psec<PROF>(pf, PR_RR);
             const bool was_walking = walking;
-            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER>(S, P.o, P.d, W, walking, stk, sb.min_ready, exhausted,
-                                                                   cnt);
+            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF>(S, P.o, P.d, W, walking, stk, sb.min_ready,
+                                                                         exhausted, cnt, &pf);
+            psec<PROF>(pf, PR_HIT);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)
             if (was_walking && !walking) {
                 fast_walk_resolve<Real, COUNT>(S, P.o, P.d, W, cnt);
                 V3 c;
                 if (path_post<Real, EMIT, COUNT, PROF>(S, C, P, W.best, W.best_t, cnt, st_err, pf, c)) finish_sample(c);
             }
+            psec<PROF>(pf, PR_ACC);
         } else if (slot >= 0) {
             const RtCamera& C = cam_opaque();
             prof_trip<PROF>(pf);
@@ -2774,6 +2799,281 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     PixStats st;
     publish_stats(out, st, st_err, lane);
     publish_counters<false, PP>(out, cnt, pf, lane);
+}
+
+
+// ---------------------------------------------------------------------------
+// Walker-pool kernel (BVH scenes: fixed spp and adaptive rounds, no emission
+// stack). The chunked kernel ties a path to a lane: its resumable walk
+// (fast_walk_rounds) runs until 48 of 64 lanes are done, then those lanes shade
+// and start their next rays - so node steps ran on ~34 of 64 lanes and the
+// shading on ~30 (tools/profile_sections.py, spheres-500). Here the 64 lanes are
+// WALKERS only, and paths live in K per-wave LDS slots with three queues:
+//   T  rays ready to trace: an idle walker takes one (its o, d) and walks it;
+//   H  walks that ended: the slot holds the closest hit (prim, exact t);
+//   N  slots that start a sample (getRay) or need a work item.
+// A wave's trip is one stage: SHADE (64 hits from H: hit record, emission,
+// scatter, the mixture-PDF light sampling of a diffuse bounce, the next level's
+// depth cut-off / roulette; a finished sample is recorded and the item's next
+// sample started on the spot), START (64 slots from N), or WALK (idle walkers
+// refill from T, then the parked-leaf walk until `min_ready` walkers are idle;
+// finished walks go to H). Walk state persists in the walkers' registers across
+// SHADE / START trips. Per path the arithmetic and draw order are path_trip's
+// (shade_hit / shade_diffuse / path_pre are the functions path_post calls, the
+// walk is fast_walk_rounds), so the sample records - and the image - are
+// bit-identical to the chunked kernel's.
+// Slot (64 B, [group][slot] float4): g0 {rng lo, rng hi, meta, hs}, g1 {o, pass
+// slot}, g2 {d, T.x}, g3 {T.y, T.z, t (double bits, H only)}; meta = (phase + 2)
+// | log2(item chunk) << 8 | (hit + 1) << 11 (H only), hs = s << 16.
+// ---------------------------------------------------------------------------
+#ifndef RT_WPOOL_BLOCK
+#define RT_WPOOL_BLOCK 512
+#endif
+constexpr int kBlockWPool = RT_WPOOL_BLOCK;
+constexpr int kWPoolSlotBytes = 64 + 3;  // four 16-byte groups + one entry in each of the three queues
+__host__ __device__ constexpr size_t wpool_wave_bytes(int K) { return ((size_t)K * kWPoolSlotBytes + 15) / 16 * 16; }
+constexpr int kWPoolMaxK = 255;  // u8 queue entries
+__device__ __forceinline__ int meta_hit(float m) { return (int)(__float_as_uint(m) >> 11) - 1; }
+
+template <class Real, int TRAV, int LDSS>
+__global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
+                                                                 SampleBuf sb) {
+    extern __shared__ int lds_stack[];
+    const RtCamera& C0 = S0.cam;
+    __shared__ PhaseRow ptab[kMaxPhases];
+    phase_table_init(sb, ptab);
+    const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
+    const int lane = threadIdx.x & (kWave - 1);
+    int* stk = lds_stack + threadIdx.x;  // this walker's stack column (stride kBlockWPool)
+    const int K = S0.wpool_k;
+    char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * wpool_wave_bytes(K);
+    float4* G = reinterpret_cast<float4*>(wpool);  // group q of slot k: G[q * K + k]
+    uint8_t* qt = reinterpret_cast<uint8_t*>(wpool + (size_t)K * 64);
+    uint8_t* qh = qt + K;
+    uint8_t* qn = qh + K;
+    const int endX = min(reg.x + reg.width, C0.width);
+    const int endY = min(reg.y + reg.height, C0.height);
+    const int n_items = sb.n_items;
+    const double rtx = 1.0 / (double)tiles_x;
+    uint32_t* cnt = nullptr;  // product build: no work counters
+    unsigned long long st_err = 0;
+    Prof pf;  // (no section timers in this kernel)
+
+    for (int k = lane; k < K; k += kWave) {
+        qn[k] = (uint8_t)k;
+        G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
+    }
+    int t_cnt = 0, h_cnt = 0, n_cnt = K;  // wave-uniform queue lengths (stacks)
+    int pool_next, pool_end;               // wave-uniform item hand-out
+    bool exhausted;
+    first_pool(sb, pool_next, pool_end, exhausted);
+    // the walker: the slot it walks (-1: idle), its walk state and ray
+    int wk = -1;
+    bool walking = false;
+    FastWalk<Real> W;
+    V3 wo = v3(0, 0, 0), wd = wo;
+
+    auto push = [&](uint8_t* q, int& c, bool want, int k) {
+        const unsigned long long m = __ballot(want);
+        if (want) {
+            const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            q[c + r] = (uint8_t)k;
+        }
+        c += __popcll(m);
+    };
+    // the sample's radiance and bounce count to its record; the slot's next phase
+    auto record = [&](V3 c, int bounces, int slot, int& s, int s_end) -> int {
+        float4 r;
+        r.x = c.x;
+        r.y = c.y;
+        r.z = c.z;
+        r.w = __int_as_float(bounces);
+        rec_store<RT_REC_NT>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
+        ++s;
+        return s < s_end ? PH_NEW : PH_ITEM;
+    };
+    // getRay for the slot's sample s, then the first level's cut-off / roulette; the
+    // phase after it: 0 (a ray to trace) or, when the path ended at once, recorded
+    auto start_path = [&](const RtCamera& C, Path<false>& P, int slot, int& s, int clog2) -> int {
+        int i, j;
+        slot_pixel(sb, reg, tiles_x, rtx, endX, endY, slot, i, j);
+        path_begin<Real, false>(C, P, pixel_center<Real>(C, i, j), (uint32_t)j * (uint32_t)C.width + (uint32_t)i,
+                                (uint32_t)(sb.s_base + s));
+        V3 c;
+        if (path_pre<Real, false, false>(C, P, pf, c)) return record(c, P.bounces, slot, s, item_end(s, clog2));
+        return 0;
+    };
+    auto store = [&](int k, const Path<false>& P, int phase, int clog2, int slot, int s) {
+        G[k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
+                           pool_meta(phase, clog2, 0), pool_hs(0, s));
+        G[K + k] = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
+        G[2 * K + k] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
+        G[3 * K + k] = make_float4(P.T.y, P.T.z, 0.f, 0.f);
+    };
+
+    while (true) {
+        // other lanes' slot and queue writes of the previous trip (one wave: LDS is in order)
+        __asm__ volatile("" ::: "memory");
+        const int nwalk = __popcll(__ballot(wk >= 0));
+        if (t_cnt + h_cnt + n_cnt + nwalk == 0) break;
+        // the stage of this trip (wave-uniform): full SHADE / START trips first, else walk
+        // while there are rays, else whatever is left
+        const int stage = h_cnt >= kWave ? 1 : n_cnt >= kWave ? 2 : (t_cnt > 0 || nwalk > 0) ? 0 : h_cnt > 0 ? 1 : 2;
+        if (stage == 0) {
+            // ---- WALK: idle walkers take rays from T, then walk ----
+            const unsigned long long idle = __ballot(wk < 0);
+            const int m = min(__popcll(idle), t_cnt);
+            if (m > 0) {
+                const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (wk < 0 && r < m) {
+                    const int k = (int)qt[t_cnt - m + r];
+                    const float4 g1 = G[K + k], g2 = G[2 * K + k];
+                    wo = V3{g1.x, g1.y, g1.z};
+                    wd = V3{g2.x, g2.y, g2.z};
+                    wk = k;
+                    fast_walk_begin<Real, false>(S, wo, wd, W, cnt);
+                    walking = true;
+                }
+                t_cnt -= m;
+            }
+            fast_walk_rounds<Real, false, TRAV == TRAV_FAST_DEFER, false, kBlockWPool>(S, wo, wd, W, walking, stk,
+                                                                                       sb.min_ready, false, cnt);
+            const bool fin = wk >= 0 && !walking;
+            if (fin) {
+                fast_walk_resolve<Real, false>(S, wo, wd, W, cnt);
+                const float4 g0 = G[wk];
+                G[wk] = make_float4(g0.x, g0.y, pool_meta(meta_phase(g0.z), meta_clog2(g0.z), W.best + 1), g0.w);
+                const float4 g3 = G[3 * K + wk];
+                float tz, tw;
+                if (sizeof(Real) == 8) {
+                    const unsigned long long tb = (unsigned long long)__double_as_longlong((double)W.best_t);
+                    tz = __uint_as_float((uint32_t)tb);
+                    tw = __uint_as_float((uint32_t)(tb >> 32));
+                } else {
+                    tz = (float)W.best_t;
+                    tw = 0.f;
+                }
+                G[3 * K + wk] = make_float4(g3.x, g3.y, tz, tw);
+            }
+            push(qh, h_cnt, fin, wk);
+            if (fin) wk = -1;
+        } else if (stage == 1) {
+            // ---- SHADE: up to 64 walked rays ----
+            const int n = min(kWave, h_cnt);
+            int k = -1;
+            if (lane < n) k = (int)qh[h_cnt - n + lane];
+            h_cnt -= n;
+            int phase = PH_ITEM;
+            if (k >= 0) {
+                const float4 g0 = G[k], g1 = G[K + k], g2 = G[2 * K + k], g3 = G[3 * K + k];
+                Path<false> P;
+                P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
+                P.bounces = meta_phase(g0.z);
+                P.em_n = 0;
+                P.o = V3{g1.x, g1.y, g1.z};
+                P.d = V3{g2.x, g2.y, g2.z};
+                P.T = V3{g2.w, g3.x, g3.y};
+                const int clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w), h = meta_hit(g0.z);
+                int s = hs_s(g0.w);
+                Real t;
+                if (sizeof(Real) == 8)
+                    t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(g3.z) |
+                                                               ((unsigned long long)__float_as_uint(g3.w) << 32)));
+                else
+                    t = (Real)g3.z;
+                const RtCamera& C = cam_opaque();
+                V3 c;
+                bool term = false;
+                if (h < 0) {
+                    term = true;
+                    c = miss_color<Real, false, false>(C, P, st_err, pf);
+                } else {
+                    V3 p, nrm, emitted, att, sdir;
+                    bool front, planar;
+                    const int kind = shade_hit<Real, false, false, false>(S, P, h, t, cnt, pf, p, nrm, front, planar,
+                                                                         emitted, att, sdir);
+                    if (kind == SC_NONE) {
+                        term = true;
+                        c = emitted;
+                    } else {
+                        ++P.bounces;
+                        if (kind == SC_SPEC) {
+                            P.T = mulv(P.T, att);
+                            P.o = p;
+                            P.d = sdir;
+                        } else if (shade_diffuse<Real, false, false, false>(S, C, P, h, planar, front, p, nrm, att, cnt,
+                                                                            pf)) {
+                            term = true;
+                            c = emitted;
+                        }
+                    }
+                }
+                if (!term) term = path_pre<Real, false, false>(C, P, pf, c);  // the next level's cut-off / roulette
+                phase = P.bounces;
+                if (term) {
+                    phase = record(c, P.bounces, slot, s, item_end(s, clog2));
+                    if (phase == PH_NEW) phase = start_path(C, P, slot, s, clog2);  // the item's next sample
+                }
+                store(k, P, phase, clog2, slot, s);
+            }
+            push(qt, t_cnt, k >= 0 && phase >= 0, k);
+            push(qn, n_cnt, k >= 0 && phase < 0, k);
+        } else {
+            // ---- START: up to 64 slots that begin a sample or need a work item ----
+            const int n = min(kWave, n_cnt);
+            int k = -1;
+            if (lane < n) k = (int)qn[n_cnt - n + lane];
+            n_cnt -= n;
+            float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f), g1 = g0;
+            if (k >= 0) {
+                g0 = G[k];
+                g1 = G[K + k];
+            }
+            int phase = meta_phase(g0.z), clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w);
+            int s = hs_s(g0.w);
+            // work items for slots without one (the chunked kernel's guided hand-out)
+            const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
+            if (need != 0ull && !exhausted) {
+                if (pool_next >= pool_end) {
+                    const int base = take_pool(out, sb, lane);
+                    if (base >= n_items) {
+                        exhausted = true;
+                    } else {
+                        pool_next = base;
+                        pool_end = min(base + sb.pool, n_items);
+                    }
+                }
+                if (!exhausted) {
+                    const int take = min(__popcll(need), pool_end - pool_next);
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                    if (k >= 0 && phase == PH_ITEM && rank < take) {
+                        int tl, l, s1, e1, i, j;
+                        item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
+                        if (slot_pixel(sb, reg, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
+                            slot = tl * 64 + l;
+                            s = s1;
+                            clog2 = __builtin_ctz((uint32_t)(e1 - s1));  // power-of-two, aligned chunks
+                            phase = PH_NEW;
+                        }
+                    }
+                    pool_next += take;
+                }
+            }
+            const bool keep = k >= 0 && (phase != PH_ITEM || !exhausted);  // drained slots leave the pool
+            if (k >= 0 && phase == PH_NEW) {
+                Path<false> P;
+                phase = start_path(cam_opaque(), P, slot, s, clog2);
+                store(k, P, phase, clog2, slot, s);
+            } else if (keep) {
+                G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);  // still waiting for a work item
+            }
+            push(qt, t_cnt, keep && phase >= 0, k);
+            push(qn, n_cnt, keep && phase < 0, k);
+        }
+    }
+    PixStats st;
+    publish_stats(out, st, st_err, lane);
 }
 
 }  // namespace rt

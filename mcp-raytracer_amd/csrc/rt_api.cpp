@@ -332,6 +332,12 @@ struct rt_camera {
                   env_flag("RT_AMD_DEFER", g.lds_level >= 1 && C.n_prims >= 100);
         if (g.lds_bytes + static_lds_bytes(count, false) > (size_t)lds_max)
             throw std::runtime_error("traversal stack exceeds the workgroup LDS (BVH too deep)");
+        if (env_flag("RT_AMD_LAUNCH_LOG", false))
+            std::fprintf(stderr,
+                         "[rt launch] prims %d stack_depth %d trav %d lds_level %d lds %zu B (stack %zu, scene L1 %d / "
+                         "L2 %d B) lds_max %d tiles %ld\n",
+                         C.n_prims, C.stack_depth, v.trav, g.lds_level, g.lds_bytes, stack, lds_words * 16,
+                         lds_words2 * 16, lds_max, mine);
         RenderOut out{rgb, rad, pxs, pxb, d_stats, d_counters, d_tile, packed ? 1 : 0};
         hip_check(launch_init_stats(d_stats, count ? d_counters : nullptr, d_tile, stream), "init_stats");
         n_passes = 0;
@@ -375,6 +381,31 @@ struct rt_camera {
                  build.prims.size() < (1u << 14) &&
                  (size_t)S.lds_pool_off + pool_lds_bytes() + static_lds_bytes(count, true) <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
+        // Walker-pool kernel (pt_wpool_kernel) for BVH scenes: 64 walkers per wave over K LDS
+        // path slots. LDS: the walkers' stacks (stride kBlockWPool), the walk data
+        // ([tnodes][tprims][tsph], level 3) when it fits, then 8 waves x K slots. RT_AMD_WPOOL=0/1.
+        int wpool_k = 0;
+        size_t wpool_lds = 0;
+        LaunchGeom gw = g;
+        if (!v.emit && count == 0 && trav_fast(v.trav) && C.width < 65536 && C.height < 65536 &&
+            C.n_samples <= 65535 && C.depth <= 250 && build.prims.size() < (1u << 20) &&
+            env_flag("RT_AMD_WPOOL", false)) {
+            const size_t wstack = (size_t)std::max(C.stack_depth, 1) * kBlockWPool * sizeof(int);
+            const size_t walk_bytes = (size_t)off_prims;  // [tnodes][tprims][tsph]: the blob's head
+            const size_t stat = static_lds_bytes(count, false);
+            gw.lds_level = lds_scene_enabled() && wstack + walk_bytes + stat <= std::min<size_t>(lds_max, kLdsSceneMaxBytes) ? 3 : 0;
+            const size_t off = (wstack + (gw.lds_level == 3 ? walk_bytes : 0) + 15) / 16 * 16;
+            const size_t per_wave = ((size_t)lds_max - stat - std::min((size_t)lds_max - stat, off)) / (kBlockWPool / kWave);
+            int k = (int)std::min<size_t>(kWPoolMaxK, per_wave >= 16 ? (per_wave - 15) / kWPoolSlotBytes : 0);
+            k = std::min(k, env_int("RT_AMD_WPOOL_K", kWPoolMaxK));
+            if (k >= 2 * kWave) {
+                wpool_k = k;
+                S.wpool_k = k;
+                S.lds_pool_off = (int32_t)off;
+                wpool_lds = off + (size_t)(kBlockWPool / kWave) * wpool_wave_bytes(k);
+                gw.lds_bytes = wpool_lds;
+            }
+        }
         // guided schedule of `nsamp` samples over `slots` pixel slots: half of the remaining
         // samples per phase, chunks halving. First-phase chunk from the samples per resident
         // lane: an item is the critical path of its pixel, so small per-launch workloads (a
@@ -383,6 +414,7 @@ struct rt_camera {
         // hand-out over long items (tools/tail_probe.py sweep).
         auto schedule = [&](double slots, int nsamp) {
             v.pool = pool_ok;
+            v.wpool = wpool_k > 0;
             // spl: samples per resident lane of this launch.
             const double spl = slots * (double)nsamp / ((double)cus * kBlockChunk);
             // Brute-force scenes in the chunked kernel: two tile-chunks per atomic from 512 spl
@@ -403,11 +435,11 @@ struct rt_camera {
             // (pool kernel, re-tuned at 152 slots per wave: 8 tile-chunks per atomic from 512 spl,
             // 4 from 48, 2 from 24, first items of at most 4 samples - Cornell N=1 14.61 -> 14.43 ms,
             // 1/2 share 7.57 -> 7.40, 1/8 share 2.57 -> 2.10 ms; profiles/r02/sched/)
-            const int pool_auto = v.pool ? (spl >= 512.0 ? 8 : spl >= 48.0 ? 4 : spl >= 24.0 ? 2 : 1)
+            const int pool_auto = (v.pool || v.wpool) ? (spl >= 512.0 ? 8 : spl >= 48.0 ? 4 : spl >= 24.0 ? 2 : 1)
                                  : bvh ? (spl >= 256.0 ? 4 : 2)
                                        : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
-            const int c_max = v.pool ? 4 : (bvh && g.lds_level == 0) ? 4 : 32;
+            const int c_max = (v.pool || v.wpool) ? 4 : (bvh && g.lds_level == 0) ? 4 : 32;
             const double c_target = bvh ? std::sqrt(spl) / 3.0 : spl / 8.0;
             int c_auto = 1;
             while (c_auto * 2 <= c_max && c_auto * 2 <= c_target) c_auto *= 2;  // pow2 floor, in [1, c_max]
@@ -438,9 +470,8 @@ struct rt_camera {
             sb.n_phases = np;
             // the pool kernel keeps log2(item chunk) in a 3-bit slot field (pool_meta): chunks
             // of more than kPoolMaxChunk samples (RT_AMD_CHUNK overrides) take the chunked kernel
-            if (v.pool)
-                for (int p = 0; p < np; ++p)
-                    if (sb.chunk[p] > kPoolMaxChunk) v.pool = false;
+            for (int p = 0; p < np; ++p)
+                if (sb.chunk[p] > kPoolMaxChunk) v.pool = v.wpool = false;
             int covered = 0;
             for (int p = 0; p < np; ++p) {
                 if (sb.s0[p] != covered) throw std::runtime_error("guided schedule: gap");
@@ -449,7 +480,7 @@ struct rt_camera {
             if (covered != nsamp) throw std::runtime_error("guided schedule: coverage");
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
-            sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
+            sb.min_ready = std::min(env_int(v.wpool ? "RT_AMD_WREADY" : "RT_AMD_READY", v.wpool ? 16 : 48), kWave);
         };
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
@@ -466,13 +497,19 @@ struct rt_camera {
             if (items >= (1l << 31) - (1l << 22)) throw std::runtime_error("chunked pass too large");  // counter headroom: 2 x grid waves x pool
             sb.n_items = (int32_t)items;
             if (!first) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
-            LaunchGeom gp = g;
-            gp.grid = (int)std::max<long>(1, std::min<long>(items / (v.pool ? kBlockPool : kBlockChunk) + 1, (long)cus));
+            LaunchGeom gp = v.wpool ? gw : g;
+            gp.grid = (int)std::max<long>(
+                1, std::min<long>(items / (v.wpool ? kBlockWPool : v.pool ? kBlockPool : kBlockChunk) + 1, (long)cus));
+            DevScene Sp = S;
             if (v.pool) gp.lds_bytes = (size_t)S.lds_pool_off + pool_lds_bytes();
+            if (v.wpool) {
+                Sp.lds_stack_bytes = (int32_t)((size_t)std::max(C.stack_depth, 1) * kBlockWPool * sizeof(int));
+                Sp.lds_words = gw.lds_level == 3 ? off_prims / 16 : 0;
+            }
             // per-pass events: path kernel [0, 1), accumulate [1, 2)
             hip_check(hipEventRecord(pass_event(pass, 0), stream), "hipEventRecord");
-            hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, S, reg, out, gp, &sb, stream)
-                                             : launch_render_ref(v, S, reg, out, gp, &sb, stream);
+            hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, Sp, reg, out, gp, &sb, stream)
+                                             : launch_render_ref(v, Sp, reg, out, gp, &sb, stream);
             hip_check(e, "pt_chunk_kernel launch");
             hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
         };
@@ -504,7 +541,7 @@ struct rt_camera {
         }
         n_passes = pass;
         ev_accum = true;
-        last_kernel = v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
+        last_kernel = v.wpool ? RT_KERNEL_WPOOL : v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
     }
 
     // Adaptive sampling in rounds (src/camera.ts:400-425). Round r renders samples
@@ -709,6 +746,16 @@ int rt_camera_create(const char* scene_json, const char* render_options_json, rt
             if (const rtj::Value* r = scene.get("render")) pick_t(r->get("traversal"));
             if (rop) pick_t(rop->get("traversal"));
             cam->traversal = trav;
+            if (env_flag("RT_AMD_LAUNCH_LOG", false)) {
+                const SceneBuild& b = cam->build;
+                std::fprintf(stderr,
+                             "[rt scene] prims %zu t4nodes %zu (%zu B) tnodes %zu tprims %zu B tsph %zu B prims %zu B "
+                             "mats %zu B lights %zu B nodes %zu stack_depth %d\n",
+                             b.prims.size(), b.t4nodes.size(), b.t4nodes.size() * sizeof(b.t4nodes[0]), b.tnodes.size(),
+                             b.tprims.size() * 4, b.tsph.size() * 16, b.prims.size() * sizeof(RtPrim),
+                             b.mats.size() * sizeof(RtMat), b.lights.size() * sizeof(RtLight), b.nodes.size(),
+                             b.cam.stack_depth);
+            }
             // MixturePDF([cosine, ...lights], [0.5, ...0.5/nL]).totalWeight (pdf.ts:48-52)
             const int nl = cam->build.cam.n_lights;
             cam->light_w = nl > 0 ? 0.5 / (double)nl : 0.0;

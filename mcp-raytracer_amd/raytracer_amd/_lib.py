@@ -22,7 +22,8 @@ TRAVERSAL = {"fast": 0, "reference": 1, "brute": 2, "auto": 3}
 
 CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_sphere",
             "bounces", "diffuse", "samples", "rays", "exact", "exact_wave", "cand0", "cand2", "exact2"]
-PR_NAMES = ["newpath", "rr", "hit", "miss", "hitrec", "scatter", "sample", "pdf", "acc", "tile", "loop", "trips"]
+PR_NAMES = ["newpath", "rr", "hit", "miss", "hitrec", "scatter", "sample", "pdf", "acc", "tile", "node", "leaf",
+            "loop", "trips"]
 COUNTER_WORDS = 64
 STATS_WORDS = 8  # RT_STATS_WORDS: pixels, samples, smin, smax, bounces, bmin, bmax, error
 

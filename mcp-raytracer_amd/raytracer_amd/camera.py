@@ -209,11 +209,11 @@ class Camera:
         _lib.check(self._lib.rt_camera_pass_count(self._h, C.byref(n)))
         return int(n.value)
 
-    KERNELS = ("none", "sequential", "chunked", "pool")
+    KERNELS = ("none", "sequential", "chunked", "pool", "wpool")
 
     def last_kernel(self) -> str:
         """Path kernel of the last render (rt_camera_last_kernel): 'sequential',
-        'chunked' or 'pool' ('none' before any)."""
+        'chunked', 'pool' or 'wpool' ('none' before any)."""
         n = C.c_int32()
         _lib.check(self._lib.rt_camera_last_kernel(self._h, C.byref(n)))
         return self.KERNELS[int(n.value)]

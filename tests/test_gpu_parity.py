@@ -871,3 +871,92 @@ def test_adaptive_full_size_headline_rows_match_oracle(rt, oracle, gpu):
         del os.environ["RT_AMD_ADAPT_ROUNDS"]
     assert_identical(rad, rgb, rad2, rgb2, "adaptive 800 rounds == sequential")
     assert st.samples == st2.samples and st.bounces == st2.bounces
+
+
+# ---------------------------------------------------------------------------
+# Walker-pool kernel (pt_wpool_kernel, BVH scenes): 64 walkers per wave over LDS
+# path slots with trace / shade / start queues. Same records as the chunked
+# kernel, so images and stats are bit-identical to it and to the oracle.
+# ---------------------------------------------------------------------------
+WPOOL_CASES = {
+    "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                {"width": 48, "aspect": 1, "samples": 8, "depth": 8, **NOADAPT}),
+    "rain": ({"type": "rain", "options": {"seed": 42}}, {"width": 64, "samples": 8, "depth": 16, **NOADAPT}),
+    "spheres_deep": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                     {"width": 40, "aspect": 1, "samples": 6, "depth": 120, **NOADAPT}),
+    "spheres_adaptive": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                         {"width": 48, "aspect": 1, "samples": 40, "depth": 8, "aTolerance": 0.1}),
+    "spheres_aperture": ({"type": "spheres", "options": {"count": 200, "seed": 7}},
+                         {"width": 40, "aspect": 1.5, "samples": 5, "depth": 10, **NOADAPT}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(WPOOL_CASES))
+def test_wpool_kernel_matches_oracle_and_chunked(rt, oracle, gpu, case, monkeypatch):
+    cfg, ro = WPOOL_CASES[case]
+    sd = rt.generate_scene_data(cfg)
+    if case == "spheres_aperture":
+        sd["camera"]["aperture"] = 0.1
+    monkeypatch.setenv("RT_AMD_WPOOL", "1")
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == "wpool"
+    orc = oracle.render(sd, ro)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wpool {case}")
+    assert_stats_identical(st, orc["stats"])
+    monkeypatch.setenv("RT_AMD_WPOOL", "0")
+    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
+    assert cam2.last_kernel() == "chunked"
+    assert_identical(rad, rgb, rad2, rgb2, f"wpool == chunked {case}")
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_wpool_random_scenes_match_oracle(rt, oracle, gpu, seed, monkeypatch):
+    sd = _random_scene(seed)
+    ro = {"width": 32, "samples": 4, "depth": 8, **NOADAPT, "traversal": "fast"}
+    orc = oracle.render(sd, ro)
+    monkeypatch.setenv("RT_AMD_WPOOL", "1")
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wpool random {seed} ({cam.last_kernel()})")
+    assert_stats_identical(st, orc["stats"])
+
+
+def test_wpool_small_pool_and_tiny_slot_counts(rt, oracle, gpu, monkeypatch):
+    """The smallest admissible pool (2 x 64 slots) and a launch with fewer pixels
+    than walkers (a 3x5 region), regions and tile groups."""
+    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 500, "seed": 42}})
+    ro = {"width": 40, "aspect": 1, "samples": 7, "depth": 8, **NOADAPT}
+    orc = oracle.render(sd, ro)
+    monkeypatch.setenv("RT_AMD_WPOOL", "1")
+    monkeypatch.setenv("RT_AMD_WPOOL_K", "128")
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == "wpool"
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], "wpool K=128")
+    monkeypatch.delenv("RT_AMD_WPOOL_K")
+    cam = rt.create_camera_from_scene_data(sd, ro)
+    rgb2 = np.zeros_like(rgb)
+    rad2 = np.zeros_like(rad)
+    cam.render_region(rgb2, (17, 11, 3, 5), radiance=rad2)
+    assert cam.last_kernel() == "wpool"
+    assert_identical(rad2[11:16, 17:20], rgb2[11:16, 17:20], orc["radiance"][11:16, 17:20], orc["rgb"][11:16, 17:20],
+                     "wpool 3x5 region")
+    assert not rgb2[:11].any() and not rgb2[16:].any()
+
+
+def test_wpool_full_size_spheres500_rows_match_oracle(rt, oracle, gpu, monkeypatch):
+    """BASELINE config 2 (spheres-500, 800x800, spp 64, depth 8) through the
+    walker pool: whole frame equal to the chunked kernel's, oracle rows exact."""
+    cfg, ro, rows = FULL["spheres"]
+    ro = {**ro, **NOADAPT}
+    sd = rt.generate_scene_data(cfg)
+    monkeypatch.setenv("RT_AMD_WPOOL", "1")
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == "wpool"
+    W, H = cam.image_width, cam.image_height
+    for y in rows:
+        orc = oracle.render(sd, ro, region=(0, y, W, 1), threads=8)
+        assert_identical(rad[y:y + 1], rgb[y:y + 1], orc["radiance"][y:y + 1], orc["rgb"][y:y + 1],
+                         f"wpool spheres-500 row {y}")
+    monkeypatch.setenv("RT_AMD_WPOOL", "0")
+    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
+    assert_identical(rad, rgb, rad2, rgb2, "wpool == chunked spheres-500 800^2")
+    assert st.bounces == st2.bounces
