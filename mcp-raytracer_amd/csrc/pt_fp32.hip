@@ -8,8 +8,8 @@ template <bool EMIT, int INSTR, int TRAV, int LDSS>
 static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
                       const SampleBuf* sb, int pk, hipStream_t stream) {
     if (sb && pk == 2) {  // walker-pool kernel: product BVH builds
-        if constexpr (!EMIT && INSTR == 0 && trav_fast(TRAV) && (LDSS == 0 || LDSS == 3)) {
-            hipLaunchKernelGGL((pt_wpool_kernel<float, TRAV, LDSS>), dim3(g.grid), dim3(kBlockWPool), g.lds_bytes,
+        if constexpr (!EMIT && INSTR != 1 && trav_fast(TRAV) && (LDSS == 0 || LDSS == 3)) {
+            hipLaunchKernelGGL((pt_wpool_kernel<float, TRAV, LDSS, INSTR == 2>), dim3(g.grid), dim3(kBlockWPool), g.lds_bytes,
                                stream, S, reg, out, g.tiles_x, *sb);
             return hipGetLastError();
         } else {

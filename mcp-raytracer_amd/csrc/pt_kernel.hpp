@@ -2835,7 +2835,7 @@ __host__ __device__ constexpr size_t wpool_wave_bytes(int K) { return ((size_t)K
 constexpr int kWPoolMaxK = 255;  // u8 queue entries
 __device__ __forceinline__ int meta_hit(float m) { return (int)(__float_as_uint(m) >> 11) - 1; }
 
-template <class Real, int TRAV, int LDSS>
+template <class Real, int TRAV, int LDSS, bool PP = false>  // PP: section timers (INSTR == 2 launches)
 __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
                                                                  SampleBuf sb) {
     extern __shared__ int lds_stack[];
@@ -2857,7 +2857,9 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
     const double rtx = 1.0 / (double)tiles_x;
     uint32_t* cnt = nullptr;  // product build: no work counters
     unsigned long long st_err = 0;
-    Prof pf;  // (no section timers in this kernel)
+    __shared__ unsigned long long prof_lds[PP ? kProfWaves * kProfSlot : 1];
+    Prof pf;
+    prof_init<PP>(pf, prof_lds, lane);
 
     for (int k = lane; k < K; k += kWave) {
         qn[k] = (uint8_t)k;
@@ -2919,6 +2921,8 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
         // the stage of this trip (wave-uniform): full SHADE / START trips first, else walk
         // while there are rays, else whatever is left
         const int stage = h_cnt >= kWave ? 1 : n_cnt >= kWave ? 2 : (t_cnt > 0 || nwalk > 0) ? 0 : h_cnt > 0 ? 1 : 2;
+        prof_trip<PP>(pf);
+        psec<PP>(pf, PR_ACC);  // the previous trip's queue appends and stage choice
         if (stage == 0) {
             // ---- WALK: idle walkers take rays from T, then walk ----
             const unsigned long long idle = __ballot(wk < 0);
@@ -2936,8 +2940,10 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 }
                 t_cnt -= m;
             }
-            fast_walk_rounds<Real, false, TRAV == TRAV_FAST_DEFER, false, kBlockWPool>(S, wo, wd, W, walking, stk,
-                                                                                       sb.min_ready, false, cnt);
+            psec<PP>(pf, PR_RR);  // refill (lanes: the walkers that took a ray)
+            fast_walk_rounds<Real, false, TRAV == TRAV_FAST_DEFER, PP, kBlockWPool>(S, wo, wd, W, walking, stk,
+                                                                                    sb.min_ready, false, cnt, &pf);
+            psec<PP>(pf, PR_HIT);
             const bool fin = wk >= 0 && !walking;
             if (fin) {
                 fast_walk_resolve<Real, false>(S, wo, wd, W, cnt);
@@ -2957,6 +2963,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             }
             push(qh, h_cnt, fin, wk);
             if (fin) wk = -1;
+            psec<PP>(pf, PR_MISS);  // finished walks to H (lanes: those walks)
         } else if (stage == 1) {
             // ---- SHADE: up to 64 walked rays ----
             const int n = min(kWave, h_cnt);
@@ -2984,14 +2991,15 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 const RtCamera& C = cam_opaque();
                 V3 c;
                 bool term = false;
+                psec<PP>(pf, PR_TILE);  // SHADE: slot loads
                 if (h < 0) {
                     term = true;
-                    c = miss_color<Real, false, false>(C, P, st_err, pf);
+                    c = miss_color<Real, false, PP>(C, P, st_err, pf);
                 } else {
                     V3 p, nrm, emitted, att, sdir;
                     bool front, planar;
-                    const int kind = shade_hit<Real, false, false, false>(S, P, h, t, cnt, pf, p, nrm, front, planar,
-                                                                         emitted, att, sdir);
+                    const int kind = shade_hit<Real, false, false, PP>(S, P, h, t, cnt, pf, p, nrm, front, planar,
+                                                                      emitted, att, sdir);
                     if (kind == SC_NONE) {
                         term = true;
                         c = emitted;
@@ -3001,8 +3009,8 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                             P.T = mulv(P.T, att);
                             P.o = p;
                             P.d = sdir;
-                        } else if (shade_diffuse<Real, false, false, false>(S, C, P, h, planar, front, p, nrm, att, cnt,
-                                                                            pf)) {
+                        } else if (shade_diffuse<Real, false, false, PP>(S, C, P, h, planar, front, p, nrm, att, cnt,
+                                                                         pf)) {
                             term = true;
                             c = emitted;
                         }
@@ -3018,6 +3026,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             }
             push(qt, t_cnt, k >= 0 && phase >= 0, k);
             push(qn, n_cnt, k >= 0 && phase < 0, k);
+            psec<PP>(pf, PR_ACC);
         } else {
             // ---- START: up to 64 slots that begin a sample or need a work item ----
             const int n = min(kWave, n_cnt);
@@ -3070,10 +3079,12 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             }
             push(qt, t_cnt, keep && phase >= 0, k);
             push(qn, n_cnt, keep && phase < 0, k);
+            psec<PP>(pf, PR_NEWPATH);  // START (hand-out and path starts)
         }
     }
     PixStats st;
     publish_stats(out, st, st_err, lane);
+    publish_counters<false, PP>(out, cnt, pf, lane);
 }
 
 }  // namespace rt

@@ -387,12 +387,12 @@ struct rt_camera {
         int wpool_k = 0;
         size_t wpool_lds = 0;
         LaunchGeom gw = g;
-        if (!v.emit && count == 0 && trav_fast(v.trav) && C.width < 65536 && C.height < 65536 &&
+        if (!v.emit && (count == 0 || (count == 2 && prec == PREC_REF)) && trav_fast(v.trav) && C.width < 65536 && C.height < 65536 &&
             C.n_samples <= 65535 && C.depth <= 250 && build.prims.size() < (1u << 20) &&
             env_flag("RT_AMD_WPOOL", false)) {
             const size_t wstack = (size_t)std::max(C.stack_depth, 1) * kBlockWPool * sizeof(int);
             const size_t walk_bytes = (size_t)off_prims;  // [tnodes][tprims][tsph]: the blob's head
-            const size_t stat = static_lds_bytes(count, false);
+            const size_t stat = static_lds_bytes(count, true);
             gw.lds_level = lds_scene_enabled() && wstack + walk_bytes + stat <= std::min<size_t>(lds_max, kLdsSceneMaxBytes) ? 3 : 0;
             const size_t off = (wstack + (gw.lds_level == 3 ? walk_bytes : 0) + 15) / 16 * 16;
             const size_t per_wave = ((size_t)lds_max - stat - std::min((size_t)lds_max - stat, off)) / (kBlockWPool / kWave);
