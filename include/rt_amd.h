@@ -92,7 +92,9 @@ typedef struct {
     int32_t* px_samples;     /* device W*H, may be NULL */
     int32_t* px_bounces;     /* device W*H, may be NULL */
     void* stream;
-    int32_t synchronize;     /* 1: wait and fill stats / work_counters; 0: asynchronous */
+    int32_t synchronize;     /* 1: wait and fill stats / work_counters; 0: asynchronous (an adaptive-
+                              * sampling render still waits on `stream` once per round: the next
+                              * round's launch is sized by the pixels left) */
     int32_t packed_tiles;    /* 0: outputs in full-frame layout; 1: tile-packed slab - the pixel
                               * of lane l (= 8*row + col inside the tile) of this launch's k-th
                               * tile at index k*64 + l (rgb/radiance 3 values per index, the

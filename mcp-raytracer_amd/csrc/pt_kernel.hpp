@@ -960,6 +960,9 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
 #ifndef RT_RESUME
 #define RT_RESUME 1
 #endif
+#ifndef RT_WALK_LEAVES
+#define RT_WALK_LEAVES 1  // leaves a walking lane parks before it idles in the node loop (1 or 2)
+#endif
 template <class Real>
 struct FastWalk {
     int ref, leaf, sp, best;
@@ -1077,13 +1080,17 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 return pop();
             };
 #endif
-            // one round of closest_hit_fast's parked-leaf walk
-            int ref = W.ref, leaf = W.leaf;
+            // one round of closest_hit_fast's parked-leaf walk (RT_WALK_LEAVES = 2: a lane
+            // parks a second leaf and keeps stepping instead of idling until the leaf phase)
+            int ref = W.ref, leaf = W.leaf, leaf2 = kTravDone;
             while (ref >= 0) {
                 if (PROF) pcount<PROF>(*pf, PR_NODE);
                 ref = node_step(ref);
                 if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
                     leaf = ref;
+                    ref = pop();
+                } else if (RT_WALK_LEAVES > 1 && ref < 0 && ref != kTravDone && leaf2 == kTravDone) {
+                    leaf2 = ref;
                     ref = pop();
                 }
                 if (__ballot(leaf == kTravDone) == 0ull) break;  // every walking lane holds a leaf
@@ -1096,7 +1103,10 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 if (PROF) pcount<PROF>(*pf, PR_LEAF);
                 leaf_test<Real, COUNT, DEFER>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
-                if (ref < 0 && ref != kTravDone) {
+                if (RT_WALK_LEAVES > 1 && leaf2 != kTravDone) {
+                    leaf = leaf2;
+                    leaf2 = kTravDone;
+                } else if (ref < 0 && ref != kTravDone) {
                     leaf = ref;
                     ref = pop();
                 }
