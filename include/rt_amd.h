@@ -232,6 +232,28 @@ int rt_tiles_unpack(const void* slabs, int32_t tile_groups, int32_t slab_tiles, 
 int rt_encode_png(const uint8_t* rgb, int32_t width, int32_t height, int32_t level, uint8_t** out, size_t* out_len);
 int rt_encode_ppm(const uint8_t* rgb, int32_t width, int32_t height, uint8_t** out, size_t* out_len);
 
+/* PNG of a DEVICE-resident u8 RGB frame (width*height*3), encoded on the GPU:
+ * per-row PNG filter (libpng's min-sum choice), the filtered stream cut into
+ * 4 KiB segments, each one deflate block with its own dynamic Huffman code
+ * (run matches at distance 1 / 3) ended by a sync flush, plus its Adler-32 and
+ * CRC-32; the host only combines those words and writes the chunk headers.
+ * Queued on `stream` (hipStream_t, NULL = default) and waited for; *out is
+ * malloc'ed (rt_free). Replaces sharp(...).png().toBuffer() (src/raytracer.ts:
+ * 101-110) without the frame crossing PCIe uncompressed. */
+int rt_encode_png_device(const uint8_t* d_rgb, int32_t width, int32_t height, void* stream, uint8_t** out,
+                         size_t* out_len);
+
+/* The same encoder run on the host, byte-identical to rt_encode_png_device
+ * (tests: the CPU pin of the device encoder's bytes). rgb: HOST pointer. */
+int rt_debug_png_host(const uint8_t* rgb, int32_t width, int32_t height, uint8_t** out, size_t* out_len);
+
+/* generateImageBuffer's core (src/raytracer.ts:39-113): renders the whole frame
+ * on the device as `bands` row bands (divideIntoRegions, src/raytracer.ts:185-205;
+ * the reference's worker split - the image does not depend on it), merges their
+ * RenderStats (RenderStats.merge) into *stats (may be NULL) and returns the PNG
+ * encoded on the device (rt_encode_png_device). *out is malloc'ed (rt_free). */
+int rt_camera_render_png(rt_camera* cam, int32_t bands, rt_render_stats* stats, uint8_t** out, size_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif

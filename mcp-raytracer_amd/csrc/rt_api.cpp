@@ -23,6 +23,9 @@
 
 using namespace rt;
 
+// png.hip: the frame's PNG, encoded on the device queue `stream` (waited for).
+std::vector<uint8_t> rt_png_encode_device(const uint8_t* d_rgb, int32_t w, int32_t h, hipStream_t stream);
+
 static_assert(ST_WORDS == RT_STATS_WORDS, "rt_camera_stats_words layout");
 
 #ifndef RT_BUILD_ID
@@ -853,6 +856,54 @@ int rt_camera_render(rt_camera* cam, uint8_t* rgb, float* radiance, rt_render_st
     if (!cam) return set_error(RT_ERR_INVALID, "null camera");
     rt_region r{0, 0, cam->build.cam.width, cam->build.cam.height};
     return rt_camera_render_region(cam, &r, rgb, radiance, stats);
+}
+
+int rt_camera_render_png(rt_camera* cam, int32_t bands, rt_render_stats* stats, uint8_t** out, size_t* out_len) {
+    if (!cam || !out || !out_len) return set_error(RT_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    try {
+        cam->ensure_device();
+        cam->ensure_frame();
+        const RtCamera& C = cam->build.cam;
+        const hipStream_t stream = nullptr;
+        // divideIntoRegions (src/raytracer.ts:185-205): ceil(H / count)-row bands
+        const int count = std::max(1, (int)bands);
+        const int rh = (C.height + count - 1) / count;
+        rt_render_stats m{};
+        m.samples_min = m.bounces_min = INFINITY;
+        for (int b = 0; b < count; ++b) {
+            const int y0 = b * rh, hh = std::min(rh, C.height - y0);
+            if (hh <= 0) break;
+            const rt_region r{0, y0, C.width, hh};
+            cam->launch(r, 0, 1, cam->precision, cam->traversal, 0, cam->d_rgb, nullptr, nullptr, nullptr, 0, stream);
+            rt_render_stats s;
+            cam->read_stats(&s, nullptr, stream);
+            // RenderStats.merge (src/render-utils/renderStats.ts:42-64)
+            m.pixels += s.pixels;
+            m.samples_total += s.samples_total;
+            m.samples_min = std::min(m.samples_min, s.samples_min);
+            m.samples_max = std::max(m.samples_max, s.samples_max);
+            m.bounces_total += s.bounces_total;
+            m.bounces_min = std::min(m.bounces_min, s.bounces_min);
+            m.bounces_max = std::max(m.bounces_max, s.bounces_max);
+        }
+        m.samples_avg = m.pixels > 0 ? m.samples_total / m.pixels : 0.0;
+        m.bounces_avg = m.samples_total > 0 ? m.bounces_total / m.samples_total : 0.0;
+        if (stats) *stats = m;
+        const std::vector<uint8_t> png = rt_png_encode_device(cam->d_rgb, C.width, C.height, stream);
+        uint8_t* b = (uint8_t*)std::malloc(png.size());
+        if (!b) throw std::runtime_error("out of memory");
+        std::memcpy(b, png.data(), png.size());
+        *out = b;
+        *out_len = png.size();
+        return RT_OK;
+    } catch (const HipError& e) {
+        return set_error(RT_ERR_DEVICE, e.what());
+    } catch (const std::invalid_argument& e) {
+        return set_error(RT_ERR_INVALID, e.what());
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_RENDER, e.what());
+    }
 }
 
 int rt_camera_render_device(rt_camera* cam, const rt_launch* L, rt_render_stats* stats, uint64_t* work_counters) {

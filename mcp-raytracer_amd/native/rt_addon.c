@@ -132,6 +132,8 @@ static int get_int_prop(napi_env env, napi_value obj, const char* key, int32_t* 
 /* renderRegion(cam, buffer: Uint8ClampedArray | Uint8Array (width*height*3, may be
  * SharedArrayBuffer-backed), region: {x, y, width, height}) -> RenderStats
  * (src/render-utils/renderStats.ts:6-19 shape). Only the region is written. */
+static napi_value stats_object(napi_env env, const rt_render_stats* s);
+
 static napi_value RenderRegion(napi_env env, napi_callback_info info) {
     size_t argc = 3;
     napi_value argv[3];
@@ -171,6 +173,12 @@ static napi_value RenderRegion(napi_env env, napi_callback_info info) {
     }
     rt_render_stats s;
     if (rt_camera_render_region(cam, &r, (uint8_t*)data, NULL, &s)) return throw_rt(env);
+    return stats_object(env, &s);
+}
+
+/* RenderStats as the reference's object shape (src/render-utils/renderStats.ts:6-19). */
+static napi_value stats_object(napi_env env, const rt_render_stats* sp) {
+    const rt_render_stats s = *sp;
     napi_value out, sm, bo;
     CHECK_NAPI(env, napi_create_object(env, &out));
     CHECK_NAPI(env, napi_create_object(env, &sm));
@@ -228,6 +236,34 @@ static napi_value EncodePng(napi_env env, napi_callback_info info) {
     return buf;
 }
 
+/* renderPng(camera, bands) -> {png: Buffer, stats}: generateImageBuffer's core
+ * (src/raytracer.ts:39-113) on the device - the frame rendered as `bands` row
+ * bands (the worker split), stats merged (RenderStats.merge), the PNG encoded on
+ * the GPU (rt_camera_render_png) so only the compressed file crosses PCIe. */
+static napi_value RenderPng(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 1) {
+        napi_throw_type_error(env, NULL, "renderPng(camera, bands)");
+        return NULL;
+    }
+    rt_camera* cam = get_camera(env, argv[0]);
+    if (!cam) return NULL;
+    int32_t bands = 1;
+    if (argc > 1) CHECK_NAPI(env, napi_get_value_int32(env, argv[1], &bands));
+    uint8_t* png = NULL;
+    size_t n = 0;
+    rt_render_stats s;
+    if (rt_camera_render_png(cam, bands, &s, &png, &n)) return throw_rt(env);
+    napi_value out, buf;
+    CHECK_NAPI(env, napi_create_object(env, &out));
+    CHECK_NAPI(env, napi_create_external_buffer(env, n, png, finalize_free, NULL, &buf));
+    napi_set_named_property(env, out, "png", buf);
+    napi_set_named_property(env, out, "stats", stats_object(env, &s));
+    return out;
+}
+
 static napi_value Version(napi_env env, napi_callback_info info) {
     (void)info;
     napi_value v;
@@ -242,6 +278,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"cameraInfo", NULL, CameraInfo, NULL, NULL, NULL, napi_default, NULL},
         {"renderRegion", NULL, RenderRegion, NULL, NULL, NULL, napi_default, NULL},
         {"encodePng", NULL, EncodePng, NULL, NULL, NULL, napi_default, NULL},
+        {"renderPng", NULL, RenderPng, NULL, NULL, NULL, napi_default, NULL},
         {"version", NULL, Version, NULL, NULL, NULL, napi_default, NULL},
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);

@@ -39,11 +39,12 @@ _UNITS = [
     ("pt_ref.hip", ["-ffp-contract=off", *_KERNEL_FLAGS], True),
     ("pt_fp32.hip", ["-ffp-contract=fast", *_KERNEL_FLAGS], True),
     ("frame.hip", [], True),
+    ("png.hip", [], True),
     ("rt_api.cpp", ["-ffp-contract=off", "-x", "hip"], True),
     ("scene.cpp", ["-ffp-contract=off"], False),
     ("image.cpp", [], False),
 ]
-_HEADERS = ["json.hpp", "rt_math.hpp", "scene.hpp", "pt_kernel.hpp", "launch.hpp"]
+_HEADERS = ["json.hpp", "rt_math.hpp", "scene.hpp", "pt_kernel.hpp", "launch.hpp", "png_deflate.hpp"]
 _LIBS = ["-lz"]
 
 

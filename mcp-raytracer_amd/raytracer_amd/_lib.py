@@ -99,6 +99,12 @@ _SIGS = {
     "rt_encode_png": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p),
                                 C.POINTER(C.c_size_t)]),
     "rt_encode_ppm": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "rt_encode_png_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_size_t)]),
+    "rt_debug_png_host": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p),
+                                    C.POINTER(C.c_size_t)]),
+    "rt_camera_render_png": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(RtRenderStats), C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_size_t)]),
 }
 
 _lib = None

@@ -145,6 +145,18 @@ class Camera:
 
     renderRegion = render_region
 
+    def render_png(self, bands: int = 1):
+        """generateImageBuffer's core on the device (rt_camera_render_png): the frame
+        rendered as `bands` row bands (divideIntoRegions; the image does not depend
+        on the split), stats merged, PNG encoded on the GPU -> (png bytes, RenderStats)."""
+        out, n = C.c_void_p(), C.c_size_t()
+        st = _lib.RtRenderStats()
+        _lib.check(self._lib.rt_camera_render_png(self._h, int(bands), C.byref(st), C.byref(out), C.byref(n)))
+        try:
+            return C.string_at(out, n.value), RenderStats._from_c(st)
+        finally:
+            self._lib.rt_free(out)
+
     def render_device(self, *, rgb_ptr=None, radiance_ptr=None, region=None, tile_group=0, tile_groups=1,
                       precision: Optional[str] = None, stream=None, synchronize=False, count_work=False,
                       px_samples_ptr=None, px_bounces_ptr=None, traversal: Optional[str] = None,

@@ -12,9 +12,7 @@ import os
 import sys
 from typing import Optional
 
-from .camera import RenderStats
-from .png import encode_png
-from .scenes import create_camera_from_scene_data, generate_scene, generate_scene_data
+from .scenes import generate_scene
 
 
 def divide_into_regions(image_width: int, image_height: int, count: int):
@@ -40,31 +38,24 @@ def generate_image_buffer(scene_config: Optional[dict] = None, options: Optional
     verbose = bool(options.get("verbose", False))
 
     camera = generate_scene(scene_config)
-    w, h, ch = camera.image_width, camera.image_height, camera.channels
-    pixel_data = bytearray(w * h * ch)
-    if not parallel:
-        stats = camera.render(pixel_data)
-    else:
-        thread_count = threads or max(1, (os.cpu_count() or 2) - 1)
+    w, h = camera.image_width, camera.image_height
+    if w * h == 0:
+        camera.close()
+        raise RuntimeError("Generated pixelData buffer is empty before calling sharp.")
+    # the reference's worker bands (parallel) or one region: rendered on the GPU into
+    # the device frame, stats merged as RenderStats.merge, PNG encoded on the GPU
+    bands = 1
+    if parallel:
+        bands = threads or max(1, (os.cpu_count() or 2) - 1)
         if verbose:
-            print(f"Starting parallel render with {thread_count} worker threads", file=sys.stderr)
-        scene_data = generate_scene_data(scene_config)
-        regions = divide_into_regions(w, h, thread_count)
-        results = []
-        for region in regions:
-            worker_cam = create_camera_from_scene_data(scene_data, scene_config.get("render"))
-            results.append(worker_cam.render_region(pixel_data, region))
-            worker_cam.close()
-        stats = RenderStats.merge(results)
+            print(f"Starting parallel render with {bands} worker threads", file=sys.stderr)
+    png, stats = camera.render_png(bands)
     camera.close()
     if verbose:
         print(f"Adaptive sampling stats: avg={stats.samples['avg']:.2f}, min={stats.samples['min']}, "
               f"max={stats.samples['max']}", file=sys.stderr)
         print(f"Ray bounce stats: avg={stats.bounces['avg']:.2f}, min={stats.bounces['min']}, "
               f"max={stats.bounces['max']}", file=sys.stderr)
-    if len(pixel_data) == 0:
-        raise RuntimeError("Generated pixelData buffer is empty before calling sharp.")
-    png = encode_png(pixel_data, w, h, ch)
     return (png, stats) if return_stats else png
 
 

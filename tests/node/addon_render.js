@@ -2,7 +2,7 @@
 // reference): the calls the reference's TypeScript host would make through
 // INTEGRATION.md's binding. usage:
 //   node addon_render.js <addon.node> info            -> JSON camera info (no GPU)
-//   node addon_render.js <addon.node> render <out.bin> -> JSON stats, RGB bytes to out.bin
+//   node addon_render.js <addon.node> render <out.bin> -> JSON stats, RGB bytes to out.bin (+ .png, .dev.png)
 //   node addon_render.js <addon.node> errors           -> JSON list of thrown messages
 'use strict';
 const fs = require('fs');
@@ -28,7 +28,10 @@ if (mode === 'info') {
   const s2 = addon.renderRegion(cam, pixels, { x: 0, y: half, width: info.imageWidth, height: info.imageHeight - half });
   fs.writeFileSync(process.argv[4], Buffer.from(shared));
   fs.writeFileSync(process.argv[4] + '.png', addon.encodePng(pixels, info.imageWidth, info.imageHeight));
-  console.log(JSON.stringify({ width: info.imageWidth, height: info.imageHeight, stats: [s1, s2] }));
+  // generateImageBuffer's core on the device: 3 worker bands, PNG encoded on the GPU
+  const dev = addon.renderPng(cam, 3);
+  fs.writeFileSync(process.argv[4] + '.dev.png', dev.png);
+  console.log(JSON.stringify({ width: info.imageWidth, height: info.imageHeight, stats: [s1, s2], devStats: dev.stats }));
 } else if (mode === 'png') {
   // host-only: encodePng of a synthetic frame (no GPU)
   const w = 5, h = 3;

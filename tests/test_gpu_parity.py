@@ -747,15 +747,44 @@ def test_packed_slabs_unpack_to_the_frame(rt, gpu, region, case, monkeypatch):
 
 
 def test_generate_image_buffer_png_pixels_equal_render(rt, gpu):
-    """PNG bytes from rt_encode_png carry exactly the rendered u8 frame."""
-    from raytracer_amd.png import decode_png_rgb
-    cfg = {"type": "cornell", "render": {"width": 32, "samples": 4, "depth": 4, "aTolerance": 0}}
-    png = rt.generate_image_buffer(cfg)
+    """generateImageBuffer's PNG (rendered and encoded on the device,
+    rt_camera_render_png) carries exactly the rendered u8 frame, is byte-identical
+    to the host run of the same encoder, and its merged stats equal a render's."""
+    from raytracer_amd.png import debug_png_host, decode_png_rgb
+    cfg = {"type": "cornell", "render": {"width": 48, "samples": 4, "depth": 4, "aTolerance": 0}}
+    png, st = rt.generate_image_buffer(cfg, {"parallel": True, "threads": 7}, return_stats=True)
     cam = rt.generate_scene(cfg)
-    rgb = np.zeros((32, 32, 3), np.uint8)
-    cam.render(rgb)
+    rgb = np.zeros((48, 48, 3), np.uint8)
+    st1 = cam.render(rgb)
     w, h, px = decode_png_rgb(png)
-    assert (w, h) == (32, 32) and px == rgb.tobytes()
+    assert (w, h) == (48, 48) and px == rgb.tobytes()
+    assert png == debug_png_host(rgb.tobytes(), 48, 48)
+    assert (st.pixels, st.samples, st.bounces) == (st1.pixels, st1.samples, st1.bounces)
+
+
+def test_device_png_encoder_matches_host_run(rt, gpu):
+    """rt_encode_png_device on frames already in HBM: the bytes equal the host run
+    of the same algorithm (rt_debug_png_host) and decode to the frame - a rendered
+    frame, noise (stored blocks), a flat frame (runs) and a 4096-wide gradient
+    whose rows span several segments."""
+    import torch
+    from raytracer_amd.png import debug_png_host, decode_png_rgb, encode_png_device
+    g = torch.Generator().manual_seed(3)
+    yy, xx = torch.meshgrid(torch.arange(40), torch.arange(4096), indexing="ij")
+    grad = torch.stack([xx % 256, (yy * 6) % 256, (xx // 16 + yy) % 256], -1).to(torch.uint8)
+    sd = rt.generate_scene_data({"type": "cornell"})
+    cam = rt.create_camera_from_scene_data(sd, {"width": 64, "samples": 8, "depth": 6, "aTolerance": 0})
+    frame = torch.zeros((64, 64, 3), dtype=torch.uint8, device="cuda")
+    cam.render_device(rgb_ptr=frame.data_ptr(), synchronize=True)
+    frames = {"render": frame.cpu(), "noise": torch.randint(0, 256, (33, 129, 3), generator=g, dtype=torch.uint8),
+              "flat": torch.full((20, 700, 3), 200, dtype=torch.uint8), "wide_gradient": grad}
+    for name, f in frames.items():
+        h, w, _ = f.shape
+        d = f.cuda().contiguous()
+        png = encode_png_device(d.data_ptr(), w, h)
+        host = f.numpy().tobytes()
+        assert png == debug_png_host(host, w, h), name
+        assert decode_png_rgb(png) == (w, h, host), name
 
 
 def test_bench_two_ranks_one_gpu_assemble_the_frame(gpu):
