@@ -60,6 +60,7 @@ struct DevScene {
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
     int32_t lds_pool_off;               // pool kernel: byte offset of the per-wave path pools (after the scene)
     int32_t wpool_k;                    // walker-pool kernel: path slots per wave (<= 255)
+    float4* __restrict__ wslots;        // walker-pool kernel: the path slots in HBM, [wave][slot][4 groups]
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
@@ -2163,6 +2164,7 @@ struct SampleBuf {
     int32_t n_items;
     int32_t refill_min;  // idle lanes that trigger a hand-out (all-idle always does)
     int32_t min_ready;   // resumable fast traversal: lanes done walking before the wave shades
+    int32_t wpolicy;     // walker-pool kernel: stage policy (0: full trips first, 1: shade when walkers starve)
     // Adaptive-sampling rounds (pt_adapt_kernel): the pass's record slot a renders the launch
     // slot act[a] (tile * 64 + lane over the launch's tiles; tile0 is 0), samples s_base + s.
     // act == nullptr: slot a is pass tile tile0 + a / 64, lane a % 64, samples from 0.
@@ -2832,18 +2834,23 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
 // (shade_hit / shade_diffuse / path_pre are the functions path_post calls, the
 // walk is fast_walk_rounds), so the sample records - and the image - are
 // bit-identical to the chunked kernel's.
-// Slot (64 B, [group][slot] float4): g0 {rng lo, rng hi, meta, hs}, g1 {o, pass
-// slot}, g2 {d, T.x}, g3 {T.y, T.z, t (double bits, H only)}; meta = (phase + 2)
-// | log2(item chunk) << 8 | (hit + 1) << 11 (H only), hs = s << 16.
+// Slot (80 B, [slot][group] float4, in HBM: the wave's K slots are a 10-20 KB run
+// that stays in L2 / MALL; LDS holds only the walkers' stacks, the walk data
+// and the three u8 queues, so the kernel runs 16 waves per CU like the chunked
+// kernel): g0 {rng lo, rng hi, meta, hs}, g1 {o, pass slot}, g2 {d, T.x}, g3
+// {T.y, T.z}, g4 {hit + 1, t (double bits)} (H only: written, never read-modified,
+// by the walker); meta = (phase + 2) | log2(item chunk) << 8, hs = s << 16. A slot is written and read by lanes
+// of one wave only; a wave's vector memory operations reach the CU's L1 and L2
+// in issue order, so a later trip's loads see an earlier trip's stores.
 // ---------------------------------------------------------------------------
 #ifndef RT_WPOOL_BLOCK
-#define RT_WPOOL_BLOCK 512
+#define RT_WPOOL_BLOCK 1024
 #endif
 constexpr int kBlockWPool = RT_WPOOL_BLOCK;
-constexpr int kWPoolSlotBytes = 64 + 3;  // four 16-byte groups + one entry in each of the three queues
-__host__ __device__ constexpr size_t wpool_wave_bytes(int K) { return ((size_t)K * kWPoolSlotBytes + 15) / 16 * 16; }
+constexpr int kWPoolSlotBytes = 80;  // five 16-byte groups (HBM)
+// LDS per wave: one entry per slot in each of the three queues
+__host__ __device__ constexpr size_t wpool_wave_bytes(int K) { return ((size_t)K * 3 + 15) / 16 * 16; }
 constexpr int kWPoolMaxK = 255;  // u8 queue entries
-__device__ __forceinline__ int meta_hit(float m) { return (int)(__float_as_uint(m) >> 11) - 1; }
 
 template <class Real, int TRAV, int LDSS, bool PP = false>  // PP: section timers (INSTR == 2 launches)
 __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
@@ -2857,8 +2864,9 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
     int* stk = lds_stack + threadIdx.x;  // this walker's stack column (stride kBlockWPool)
     const int K = S0.wpool_k;
     char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * wpool_wave_bytes(K);
-    float4* G = reinterpret_cast<float4*>(wpool);  // group q of slot k: G[q * K + k]
-    uint8_t* qt = reinterpret_cast<uint8_t*>(wpool + (size_t)K * 64);
+    // group q of slot k: G[5 * k + q]
+    float4* G = S0.wslots + (size_t)(blockIdx.x * (kBlockWPool / kWave) + threadIdx.x / kWave) * (size_t)K * 5;
+    uint8_t* qt = reinterpret_cast<uint8_t*>(wpool);
     uint8_t* qh = qt + K;
     uint8_t* qn = qh + K;
     const int endX = min(reg.x + reg.width, C0.width);
@@ -2873,7 +2881,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
 
     for (int k = lane; k < K; k += kWave) {
         qn[k] = (uint8_t)k;
-        G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
+        G[5 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
     }
     int t_cnt = 0, h_cnt = 0, n_cnt = K;  // wave-uniform queue lengths (stacks)
     int pool_next, pool_end;               // wave-uniform item hand-out
@@ -2916,11 +2924,11 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
         return 0;
     };
     auto store = [&](int k, const Path<false>& P, int phase, int clog2, int slot, int s) {
-        G[k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
+        G[5 * k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
                            pool_meta(phase, clog2, 0), pool_hs(0, s));
-        G[K + k] = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
-        G[2 * K + k] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
-        G[3 * K + k] = make_float4(P.T.y, P.T.z, 0.f, 0.f);
+        G[5 * k + 1] = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
+        G[5 * k + 2] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
+        G[5 * k + 3] = make_float4(P.T.y, P.T.z, 0.f, 0.f);
     };
 
     while (true) {
@@ -2930,7 +2938,13 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
         if (t_cnt + h_cnt + n_cnt + nwalk == 0) break;
         // the stage of this trip (wave-uniform): full SHADE / START trips first, else walk
         // while there are rays, else whatever is left
-        const int stage = h_cnt >= kWave ? 1 : n_cnt >= kWave ? 2 : (t_cnt > 0 || nwalk > 0) ? 0 : h_cnt > 0 ? 1 : 2;
+        // policy 1: when the idle walkers outnumber the rays to trace, shade / start what is
+        // there (a partial trip) rather than walk on with idle lanes
+        const bool starve = sb.wpolicy != 0 && t_cnt < kWave - nwalk && kWave - nwalk >= sb.min_ready &&
+                            (h_cnt > 0 || n_cnt > 0);
+        const int stage = h_cnt >= kWave ? 1 : n_cnt >= kWave ? 2
+                        : (!starve && (t_cnt > 0 || nwalk > 0)) ? 0
+                        : (h_cnt > 0 && h_cnt >= n_cnt) ? 1 : n_cnt > 0 ? 2 : h_cnt > 0 ? 1 : 0;
         prof_trip<PP>(pf);
         psec<PP>(pf, PR_ACC);  // the previous trip's queue appends and stage choice
         if (stage == 0) {
@@ -2941,7 +2955,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 if (wk < 0 && r < m) {
                     const int k = (int)qt[t_cnt - m + r];
-                    const float4 g1 = G[K + k], g2 = G[2 * K + k];
+                    const float4 g1 = G[5 * k + 1], g2 = G[5 * k + 2];
                     wo = V3{g1.x, g1.y, g1.z};
                     wd = V3{g2.x, g2.y, g2.z};
                     wk = k;
@@ -2957,9 +2971,6 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             const bool fin = wk >= 0 && !walking;
             if (fin) {
                 fast_walk_resolve<Real, false>(S, wo, wd, W, cnt);
-                const float4 g0 = G[wk];
-                G[wk] = make_float4(g0.x, g0.y, pool_meta(meta_phase(g0.z), meta_clog2(g0.z), W.best + 1), g0.w);
-                const float4 g3 = G[3 * K + wk];
                 float tz, tw;
                 if (sizeof(Real) == 8) {
                     const unsigned long long tb = (unsigned long long)__double_as_longlong((double)W.best_t);
@@ -2969,7 +2980,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                     tz = (float)W.best_t;
                     tw = 0.f;
                 }
-                G[3 * K + wk] = make_float4(g3.x, g3.y, tz, tw);
+                G[5 * wk + 4] = make_float4(__int_as_float(W.best + 1), tz, tw, 0.f);
             }
             push(qh, h_cnt, fin, wk);
             if (fin) wk = -1;
@@ -2982,7 +2993,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             h_cnt -= n;
             int phase = PH_ITEM;
             if (k >= 0) {
-                const float4 g0 = G[k], g1 = G[K + k], g2 = G[2 * K + k], g3 = G[3 * K + k];
+                const float4 g0 = G[5 * k], g1 = G[5 * k + 1], g2 = G[5 * k + 2], g3 = G[5 * k + 3], g4 = G[5 * k + 4];
                 Path<false> P;
                 P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
                 P.bounces = meta_phase(g0.z);
@@ -2990,14 +3001,14 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 P.o = V3{g1.x, g1.y, g1.z};
                 P.d = V3{g2.x, g2.y, g2.z};
                 P.T = V3{g2.w, g3.x, g3.y};
-                const int clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w), h = meta_hit(g0.z);
+                const int clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w), h = __float_as_int(g4.x) - 1;
                 int s = hs_s(g0.w);
                 Real t;
                 if (sizeof(Real) == 8)
-                    t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(g3.z) |
-                                                               ((unsigned long long)__float_as_uint(g3.w) << 32)));
+                    t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(g4.y) |
+                                                               ((unsigned long long)__float_as_uint(g4.z) << 32)));
                 else
-                    t = (Real)g3.z;
+                    t = (Real)g4.y;
                 const RtCamera& C = cam_opaque();
                 V3 c;
                 bool term = false;
@@ -3045,8 +3056,8 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             n_cnt -= n;
             float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f), g1 = g0;
             if (k >= 0) {
-                g0 = G[k];
-                g1 = G[K + k];
+                g0 = G[5 * k];
+                g1 = G[5 * k + 1];
             }
             int phase = meta_phase(g0.z), clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w);
             int s = hs_s(g0.w);
@@ -3085,7 +3096,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 phase = start_path(cam_opaque(), P, slot, s, clog2);
                 store(k, P, phase, clog2, slot, s);
             } else if (keep) {
-                G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);  // still waiting for a work item
+                G[5 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);  // still waiting for a work item
             }
             push(qt, t_cnt, keep && phase >= 0, k);
             push(qn, n_cnt, keep && phase < 0, k);

@@ -141,7 +141,7 @@ struct rt_camera {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         for (void* p : {(void*)d_blob, (void*)d_stats, (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad,
-                        (void*)d_sbuf})
+                        (void*)d_sbuf, (void*)d_wslots})
             if (p) (void)hipFree(p);
         // every freed pointer is reset: a later ensure_device / ensure_frame /
         // ensure_sbuf (possibly on another device) must reallocate all of them
@@ -153,6 +153,8 @@ struct rt_camera {
         d_rad = nullptr;
         d_sbuf = nullptr;
         sbuf_cap = 0;
+        d_wslots = nullptr;
+        wslots_cap = 0;
         free_adapt_buffers();
         if (d_acount) (void)hipFree(d_acount);
         d_acount = nullptr;
@@ -285,6 +287,9 @@ struct rt_camera {
         S.off_mats = off_mats;
         S.off_lights = off_lights;
         S.lds_stack_bytes = 0;
+        S.lds_pool_off = 0;
+        S.wpool_k = 0;
+        S.wslots = nullptr;
         S.troot = RT_BVH4 ? build.t4root : build.troot;
         S.root_box = build.troot_box;
         S.cam = build.cam;
@@ -384,29 +389,29 @@ struct rt_camera {
                  build.prims.size() < (1u << 14) &&
                  (size_t)S.lds_pool_off + pool_lds_bytes() + static_lds_bytes(count, true) <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
-        // Walker-pool kernel (pt_wpool_kernel) for BVH scenes: 64 walkers per wave over K LDS
-        // path slots. LDS: the walkers' stacks (stride kBlockWPool), the walk data
-        // ([tnodes][tprims][tsph], level 3) when it fits, then 8 waves x K slots. RT_AMD_WPOOL=0/1.
+        // Walker-pool kernel (pt_wpool_kernel) for BVH scenes: 64 walkers per wave over K path
+        // slots in HBM. LDS: the walkers' stacks (stride kBlockWPool), the walk data
+        // ([tnodes][tprims][tsph], level 3) when it fits, then the waves' u8 queues. RT_AMD_WPOOL=0/1.
         int wpool_k = 0;
-        size_t wpool_lds = 0;
         LaunchGeom gw = g;
         if (!v.emit && (count == 0 || (count == 2 && prec == PREC_REF)) && trav_fast(v.trav) && C.width < 65536 && C.height < 65536 &&
             C.n_samples <= 65535 && C.depth <= 250 && build.prims.size() < (1u << 20) &&
             env_flag("RT_AMD_WPOOL", false)) {
+            const int k = std::max(2 * kWave, std::min(env_int("RT_AMD_WPOOL_K", 192), kWPoolMaxK));
             const size_t wstack = (size_t)std::max(C.stack_depth, 1) * kBlockWPool * sizeof(int);
             const size_t walk_bytes = (size_t)off_prims;  // [tnodes][tprims][tsph]: the blob's head
             const size_t stat = static_lds_bytes(count, true);
-            gw.lds_level = lds_scene_enabled() && wstack + walk_bytes + stat <= std::min<size_t>(lds_max, kLdsSceneMaxBytes) ? 3 : 0;
+            const size_t queues = (size_t)(kBlockWPool / kWave) * wpool_wave_bytes(k);
+            const size_t cap = std::min<size_t>(lds_max, kLdsSceneMaxBytes);
+            gw.lds_level = lds_scene_enabled() && wstack + walk_bytes + queues + stat + 16 <= cap ? 3 : 0;
             const size_t off = (wstack + (gw.lds_level == 3 ? walk_bytes : 0) + 15) / 16 * 16;
-            const size_t per_wave = ((size_t)lds_max - stat - std::min((size_t)lds_max - stat, off)) / (kBlockWPool / kWave);
-            int k = (int)std::min<size_t>(kWPoolMaxK, per_wave >= 16 ? (per_wave - 15) / kWPoolSlotBytes : 0);
-            k = std::min(k, env_int("RT_AMD_WPOOL_K", kWPoolMaxK));
-            if (k >= 2 * kWave) {
+            if (off + queues + stat <= (size_t)lds_max) {
                 wpool_k = k;
                 S.wpool_k = k;
                 S.lds_pool_off = (int32_t)off;
-                wpool_lds = off + (size_t)(kBlockWPool / kWave) * wpool_wave_bytes(k);
-                gw.lds_bytes = wpool_lds;
+                gw.lds_bytes = off + queues;
+                ensure_wslots((size_t)cus * (kBlockWPool / kWave) * (size_t)k * kWPoolSlotBytes);
+                S.wslots = d_wslots;
             }
         }
         // guided schedule of `nsamp` samples over `slots` pixel slots: half of the remaining
@@ -484,6 +489,7 @@ struct rt_camera {
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int(v.wpool ? "RT_AMD_WREADY" : "RT_AMD_READY", v.wpool ? 16 : 48), kWave);
+            sb.wpolicy = env_int("RT_AMD_WPOLICY", 1);
         };
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
@@ -643,6 +649,17 @@ struct rt_camera {
     // Per-sample record buffer of the chunked kernel (grown on demand, kept).
     float4* d_sbuf = nullptr;
     size_t sbuf_cap = 0;
+    // walker-pool kernel: the path slots of every resident wave (HBM)
+    float4* d_wslots = nullptr;
+    size_t wslots_cap = 0;
+    void ensure_wslots(size_t bytes) {
+        if (bytes <= wslots_cap) return;
+        if (d_wslots) (void)hipFree(d_wslots);
+        d_wslots = nullptr;
+        wslots_cap = 0;
+        hip_check(hipMalloc(&d_wslots, bytes), "hipMalloc(walker-pool slots)");
+        wslots_cap = bytes;
+    }
     void ensure_sbuf(size_t bytes) {
         if (bytes <= sbuf_cap) return;
         if (d_sbuf) (void)hipFree(d_sbuf);
