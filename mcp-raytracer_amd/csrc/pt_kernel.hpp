@@ -2164,6 +2164,7 @@ struct SampleBuf {
     int32_t n_items;
     int32_t refill_min;  // idle lanes that trigger a hand-out (all-idle always does)
     int32_t min_ready;   // resumable fast traversal: lanes done walking before the wave shades
+    int32_t tail_from, tail_pool;  // the launch's last items [tail_from, n_items): takes of tail_pool items
     int32_t wpolicy;     // walker-pool kernel: stage policy (0: full trips first, 1: shade when walkers starve)
     // Adaptive-sampling rounds (pt_adapt_kernel): the pass's record slot a renders the launch
     // slot act[a] (tile * 64 + lane over the launch's tiles; tile0 is 0), samples s_base + s.
@@ -2290,10 +2291,32 @@ __device__ __forceinline__ void first_pool(const SampleBuf& sb, int& pool_next, 
     pool_end = min(pool_next + sb.pool, sb.n_items);
     exhausted = pool_next >= sb.n_items;
 }
-__device__ __forceinline__ int take_pool(const RenderOut& out, const SampleBuf& sb, int lane) {
+// A wave's next item range [pool_next, pool_end) (wave-uniform; exhausted when none is
+// left). Items below sb.tail_from come from the first counter in takes of sb.pool items;
+// the launch's last items [tail_from, n_items) from a second counter in takes of
+// sb.tail_pool, so the waves that draw the last items hold less of them (the drain).
+__device__ __forceinline__ void take_pool(const RenderOut& out, const SampleBuf& sb, int lane, int& pool_next,
+                                          int& pool_end, bool& exhausted) {
+    if (pool_next < sb.tail_from) {
+        int base = 0;
+        if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64)) + (int)(gridDim.x * (blockDim.x / kWave)) * sb.pool;
+        if (base < sb.tail_from) {
+            pool_next = base;
+            pool_end = min(base + sb.pool, sb.tail_from);
+            return;
+        }
+    }
     int base = 0;
-    if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
-    return __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64)) + (int)(gridDim.x * (blockDim.x / kWave)) * sb.pool;
+    if (lane == 0) base = (int)atomicAdd(out.tile_counter + 1, (unsigned)sb.tail_pool);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64)) + sb.tail_from;
+    if (base >= sb.n_items) {
+        exhausted = true;
+        pool_next = pool_end = sb.n_items;
+        return;
+    }
+    pool_next = base;
+    pool_end = min(base + sb.tail_pool, sb.n_items);
 }
 
 template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
@@ -2344,15 +2367,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
         const unsigned long long need = __ballot(slot < 0);
         const int n_need = __popcll(need);
         if (n_need != 0 && !exhausted && (n_need >= sb.refill_min || __ballot(slot >= 0) == 0ull)) {
-            if (pool_next >= pool_end) {
-                const int base = take_pool(out, sb, lane);
-                if (base >= n_items) {
-                    exhausted = true;
-                } else {
-                    pool_next = base;
-                    pool_end = min(base + sb.pool, n_items);
-                }
-            }
+            if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
             if (!exhausted) {
                 const int take = min(n_need, pool_end - pool_next);
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -2688,15 +2703,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
             // work items for slots without one (the chunked kernel's guided hand-out)
             const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
             if (need != 0ull && !exhausted) {
-                if (pool_next >= pool_end) {
-                    const int base = take_pool(out, sb, lane);
-                    if (base >= n_items) {
-                        exhausted = true;
-                    } else {
-                        pool_next = base;
-                        pool_end = min(base + sb.pool, n_items);
-                    }
-                }
+                if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
                 if (!exhausted) {
                     const int take = min(__popcll(need), pool_end - pool_next);
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -2834,12 +2841,14 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
 // (shade_hit / shade_diffuse / path_pre are the functions path_post calls, the
 // walk is fast_walk_rounds), so the sample records - and the image - are
 // bit-identical to the chunked kernel's.
-// Slot (80 B, [slot][group] float4, in HBM: the wave's K slots are a 10-20 KB run
+// Slot (64 B, [slot][group] float4, in HBM: the wave's K slots are an 8-16 KB run
 // that stays in L2 / MALL; LDS holds only the walkers' stacks, the walk data
 // and the three u8 queues, so the kernel runs 16 waves per CU like the chunked
 // kernel): g0 {rng lo, rng hi, meta, hs}, g1 {o, pass slot}, g2 {d, T.x}, g3
-// {T.y, T.z}, g4 {hit + 1, t (double bits)} (H only: written, never read-modified,
-// by the walker); meta = (phase + 2) | log2(item chunk) << 8, hs = s << 16. A slot is written and read by lanes
+// {T.y, T.z, t (double bits, H only)}; meta = (phase + 2) | log2(item chunk) << 8
+// | (hit + 1) << 11 (H only), hs = s << 16. (An 80-byte slot with a write-only hit
+// group instead of the two read-modify-writes ran slower: 6.88 vs 6.57 ms on
+// spheres-500, profiles/r03/wpool_hbm/.) A slot is written and read by lanes
 // of one wave only; a wave's vector memory operations reach the CU's L1 and L2
 // in issue order, so a later trip's loads see an earlier trip's stores.
 // ---------------------------------------------------------------------------
@@ -2847,7 +2856,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
 #define RT_WPOOL_BLOCK 1024
 #endif
 constexpr int kBlockWPool = RT_WPOOL_BLOCK;
-constexpr int kWPoolSlotBytes = 80;  // five 16-byte groups (HBM)
+constexpr int kWPoolSlotBytes = 64;  // four 16-byte groups (HBM)
 // LDS per wave: one entry per slot in each of the three queues
 __host__ __device__ constexpr size_t wpool_wave_bytes(int K) { return ((size_t)K * 3 + 15) / 16 * 16; }
 constexpr int kWPoolMaxK = 255;  // u8 queue entries
@@ -2864,8 +2873,8 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
     int* stk = lds_stack + threadIdx.x;  // this walker's stack column (stride kBlockWPool)
     const int K = S0.wpool_k;
     char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * wpool_wave_bytes(K);
-    // group q of slot k: G[5 * k + q]
-    float4* G = S0.wslots + (size_t)(blockIdx.x * (kBlockWPool / kWave) + threadIdx.x / kWave) * (size_t)K * 5;
+    // group q of slot k: G[4 * k + q]
+    float4* G = S0.wslots + (size_t)(blockIdx.x * (kBlockWPool / kWave) + threadIdx.x / kWave) * (size_t)K * 4;
     uint8_t* qt = reinterpret_cast<uint8_t*>(wpool);
     uint8_t* qh = qt + K;
     uint8_t* qn = qh + K;
@@ -2881,7 +2890,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
 
     for (int k = lane; k < K; k += kWave) {
         qn[k] = (uint8_t)k;
-        G[5 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
+        G[4 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
     }
     int t_cnt = 0, h_cnt = 0, n_cnt = K;  // wave-uniform queue lengths (stacks)
     int pool_next, pool_end;               // wave-uniform item hand-out
@@ -2924,11 +2933,11 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
         return 0;
     };
     auto store = [&](int k, const Path<false>& P, int phase, int clog2, int slot, int s) {
-        G[5 * k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
+        G[4 * k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
                            pool_meta(phase, clog2, 0), pool_hs(0, s));
-        G[5 * k + 1] = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
-        G[5 * k + 2] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
-        G[5 * k + 3] = make_float4(P.T.y, P.T.z, 0.f, 0.f);
+        G[4 * k + 1] = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
+        G[4 * k + 2] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
+        G[4 * k + 3] = make_float4(P.T.y, P.T.z, 0.f, 0.f);
     };
 
     while (true) {
@@ -2955,7 +2964,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 if (wk < 0 && r < m) {
                     const int k = (int)qt[t_cnt - m + r];
-                    const float4 g1 = G[5 * k + 1], g2 = G[5 * k + 2];
+                    const float4 g1 = G[4 * k + 1], g2 = G[4 * k + 2];
                     wo = V3{g1.x, g1.y, g1.z};
                     wd = V3{g2.x, g2.y, g2.z};
                     wk = k;
@@ -2980,7 +2989,10 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                     tz = (float)W.best_t;
                     tw = 0.f;
                 }
-                G[5 * wk + 4] = make_float4(__int_as_float(W.best + 1), tz, tw, 0.f);
+                const float4 g0 = G[4 * wk];
+                G[4 * wk] = make_float4(g0.x, g0.y, pool_meta(meta_phase(g0.z), meta_clog2(g0.z), W.best + 1), g0.w);
+                const float4 g3 = G[4 * wk + 3];
+                G[4 * wk + 3] = make_float4(g3.x, g3.y, tz, tw);
             }
             push(qh, h_cnt, fin, wk);
             if (fin) wk = -1;
@@ -2993,7 +3005,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             h_cnt -= n;
             int phase = PH_ITEM;
             if (k >= 0) {
-                const float4 g0 = G[5 * k], g1 = G[5 * k + 1], g2 = G[5 * k + 2], g3 = G[5 * k + 3], g4 = G[5 * k + 4];
+                const float4 g0 = G[4 * k], g1 = G[4 * k + 1], g2 = G[4 * k + 2], g3 = G[4 * k + 3];
                 Path<false> P;
                 P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
                 P.bounces = meta_phase(g0.z);
@@ -3001,14 +3013,14 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 P.o = V3{g1.x, g1.y, g1.z};
                 P.d = V3{g2.x, g2.y, g2.z};
                 P.T = V3{g2.w, g3.x, g3.y};
-                const int clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w), h = __float_as_int(g4.x) - 1;
+                const int clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w), h = (int)(__float_as_uint(g0.z) >> 11) - 1;
                 int s = hs_s(g0.w);
                 Real t;
                 if (sizeof(Real) == 8)
-                    t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(g4.y) |
-                                                               ((unsigned long long)__float_as_uint(g4.z) << 32)));
+                    t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(g3.z) |
+                                                               ((unsigned long long)__float_as_uint(g3.w) << 32)));
                 else
-                    t = (Real)g4.y;
+                    t = (Real)g3.z;
                 const RtCamera& C = cam_opaque();
                 V3 c;
                 bool term = false;
@@ -3056,23 +3068,15 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
             n_cnt -= n;
             float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f), g1 = g0;
             if (k >= 0) {
-                g0 = G[5 * k];
-                g1 = G[5 * k + 1];
+                g0 = G[4 * k];
+                g1 = G[4 * k + 1];
             }
             int phase = meta_phase(g0.z), clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w);
             int s = hs_s(g0.w);
             // work items for slots without one (the chunked kernel's guided hand-out)
             const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
             if (need != 0ull && !exhausted) {
-                if (pool_next >= pool_end) {
-                    const int base = take_pool(out, sb, lane);
-                    if (base >= n_items) {
-                        exhausted = true;
-                    } else {
-                        pool_next = base;
-                        pool_end = min(base + sb.pool, n_items);
-                    }
-                }
+                if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
                 if (!exhausted) {
                     const int take = min(__popcll(need), pool_end - pool_next);
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -3096,7 +3100,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
                 phase = start_path(cam_opaque(), P, slot, s, clog2);
                 store(k, P, phase, clog2, slot, s);
             } else if (keep) {
-                G[5 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);  // still waiting for a work item
+                G[4 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);  // still waiting for a work item
             }
             push(qt, t_cnt, keep && phase >= 0, k);
             push(qn, n_cnt, keep && phase < 0, k);

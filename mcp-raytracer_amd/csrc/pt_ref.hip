@@ -71,7 +71,7 @@ __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long*
     const int t = threadIdx.x;
     if (t < ST_WORDS) stats[t * kStatStride] = (t == ST_SMIN || t == ST_BMIN) ? ~0ull : 0ull;
     if (counters && t < kCounterWords) counters[t] = 0ull;
-    if (t == 0) *tile_counter = 0u;
+    if (t < 2) tile_counter[t] = 0u;  // bulk and tail item counters
 }
 
 constexpr int kAccBlock = 256;

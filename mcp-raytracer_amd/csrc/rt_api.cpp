@@ -397,7 +397,7 @@ struct rt_camera {
         if (!v.emit && (count == 0 || (count == 2 && prec == PREC_REF)) && trav_fast(v.trav) && C.width < 65536 && C.height < 65536 &&
             C.n_samples <= 65535 && C.depth <= 250 && build.prims.size() < (1u << 20) &&
             env_flag("RT_AMD_WPOOL", false)) {
-            const int k = std::max(2 * kWave, std::min(env_int("RT_AMD_WPOOL_K", 192), kWPoolMaxK));
+            const int k = std::max(2 * kWave, std::min(env_int("RT_AMD_WPOOL_K", 128), kWPoolMaxK));
             const size_t wstack = (size_t)std::max(C.stack_depth, 1) * kBlockWPool * sizeof(int);
             const size_t walk_bytes = (size_t)off_prims;  // [tnodes][tprims][tsph]: the blob's head
             const size_t stat = static_lds_bytes(count, true);
@@ -489,7 +489,7 @@ struct rt_camera {
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int(v.wpool ? "RT_AMD_WREADY" : "RT_AMD_READY", v.wpool ? 16 : 48), kWave);
-            sb.wpolicy = env_int("RT_AMD_WPOLICY", 1);
+            sb.wpolicy = env_int("RT_AMD_WPOLICY", 0);  // policy 1 measured within noise (profiles/r03/wpool_hbm/)
         };
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
@@ -505,10 +505,17 @@ struct rt_camera {
             }
             if (items >= (1l << 31) - (1l << 22)) throw std::runtime_error("chunked pass too large");  // counter headroom: 2 x grid waves x pool
             sb.n_items = (int32_t)items;
-            if (!first) hip_check(hipMemsetAsync(d_tile, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
+            if (!first) hip_check(hipMemsetAsync(d_tile, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = v.wpool ? gw : g;
-            gp.grid = (int)std::max<long>(
-                1, std::min<long>(items / (v.wpool ? kBlockWPool : v.pool ? kBlockPool : kBlockChunk) + 1, (long)cus));
+            const int block = v.wpool ? kBlockWPool : v.pool ? kBlockPool : kBlockChunk;
+            gp.grid = (int)std::max<long>(1, std::min<long>(items / block + 1, (long)cus));
+            // the launch's last RT_AMD_TAIL rounds of takes (one round = every resident wave
+            // taking sb.pool items) come in takes of RT_AMD_TAIL_POOL tile-chunks
+            const long gwaves = (long)gp.grid * (block / kWave);
+            const long static_end = std::min<long>(gwaves * sb.pool, items);
+            const long tail_items = (long)std::max(env_int("RT_AMD_TAIL", 0), 0) * gwaves * sb.pool;
+            sb.tail_from = (int32_t)std::min<long>(items, std::max<long>(static_end, items - tail_items));
+            sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 1));
             DevScene Sp = S;
             if (v.pool) gp.lds_bytes = (size_t)S.lds_pool_off + pool_lds_bytes();
             if (v.wpool) {
