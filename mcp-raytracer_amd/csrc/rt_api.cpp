@@ -509,13 +509,17 @@ struct rt_camera {
             LaunchGeom gp = v.wpool ? gw : g;
             const int block = v.wpool ? kBlockWPool : v.pool ? kBlockPool : kBlockChunk;
             gp.grid = (int)std::max<long>(1, std::min<long>(items / block + 1, (long)cus));
-            // the launch's last RT_AMD_TAIL rounds of takes (one round = every resident wave
-            // taking sb.pool items) come in takes of RT_AMD_TAIL_POOL tile-chunks
+            // the launch's last items - RT_AMD_TAIL quarter-rounds of takes, one round = every
+            // resident wave taking sb.pool items - come in takes of RT_AMD_TAIL_POOL tile-chunks
+            // from a second counter: the waves that draw the last items hold fewer of them.
+            // One round in 2-tile-chunk takes: Cornell rank shares N=1 15.38 -> 15.20 ms, N=8
+            // 2.27 -> 2.20; spheres-500 N=8 1.136 -> 1.089 ms (1-tile-chunk takes: no change,
+            // two rounds: slower; profiles/r03/tail/)
             const long gwaves = (long)gp.grid * (block / kWave);
             const long static_end = std::min<long>(gwaves * sb.pool, items);
-            const long tail_items = (long)std::max(env_int("RT_AMD_TAIL", 0), 0) * gwaves * sb.pool;
+            const long tail_items = (long)std::max(env_int("RT_AMD_TAIL", 4), 0) * gwaves * sb.pool / 4;
             sb.tail_from = (int32_t)std::min<long>(items, std::max<long>(static_end, items - tail_items));
-            sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 1));
+            sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 2));
             DevScene Sp = S;
             if (v.pool) gp.lds_bytes = (size_t)S.lds_pool_off + pool_lds_bytes();
             if (v.wpool) {

@@ -5,9 +5,9 @@ cd ${GRAFT_REPO_ROOT:-$(pwd)}
 O=gpurun_out/${TAG:-tail}
 mkdir -p $O
 ARMS=${ARMS:-"base RT_AMD_TAIL=0
-t1p1 RT_AMD_TAIL=1 RT_AMD_TAIL_POOL=1
-t2p1 RT_AMD_TAIL=2 RT_AMD_TAIL_POOL=1
-t1p2 RT_AMD_TAIL=1 RT_AMD_TAIL_POOL=2"}
+t1p1 RT_AMD_TAIL=4 RT_AMD_TAIL_POOL=1
+t2p1 RT_AMD_TAIL=8 RT_AMD_TAIL_POOL=1
+t1p2 RT_AMD_TAIL=4 RT_AMD_TAIL_POOL=2"}
 echo "$ARMS" | while read -r arm envs; do
   [ -z "$arm" ] && continue
   for sc in cornell spheres; do
