@@ -53,6 +53,12 @@ hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut&
 // One adaptive-sampling round's accumulate / convergence pass over the pass's slots.
 hipError_t launch_adapt(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
                         const SampleBuf& sb, const AdaptRound& ar, hipStream_t stream);
+// Wavefront passes (ref precision, fast traversal): slot init, then one shade + trace
+// iteration (pt_kernel.hpp wf_shade_kernel / wf_trace_kernel).
+hipError_t launch_wf_init(const WfState& W, const SampleBuf& sb, hipStream_t stream);
+hipError_t launch_wf_iteration(bool defer, const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
+                               const SampleBuf& sb, const WfState& W, int it, int trace_grid, size_t trace_lds,
+                               hipStream_t stream);
 // Resets the stats words / counters / tile counter before a render.
 hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* counters, unsigned int* tile_counter,
                              hipStream_t stream);

@@ -3112,4 +3112,237 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
     publish_counters<false, PP>(out, cnt, pf, lane);
 }
 
+
+// ---------------------------------------------------------------------------
+// Wavefront passes for large BVH launches (trees walked from global memory,
+// e.g. spheres-100k / BASELINE config 5). In the chunked kernel a lane owns a
+// path through its whole walk; the walk is ~83 % of the time, bound by the
+// dependent node fetches of lanes that are mostly idle (node steps on ~27 of 64
+// lanes) at 4 waves per SIMD, because the shading code's registers cap the
+// occupancy. Here the pass's paths live in WfState's HBM slots and every
+// iteration runs two kernels:
+//   wf_shade_kernel (one lane per slot): the rest of the level of the ray traced
+//     last iteration (path_post: miss, emission, scatter, mixture-PDF light
+//     sampling), the sample record when the path ends, the item hand-out and the
+//     next sample's getRay (path_begin), and the next level's depth cut-off /
+//     roulette (path_pre); it flags the slots that have a ray to trace;
+//   wf_trace_kernel (walk only, <= 96 VGPRs, 5 waves per SIMD): each wave owns a
+//     contiguous run of slots; idle lanes take the next flagged slots (ballot +
+//     rank compaction through LDS) and walk them (fast_walk_rounds); a walk that
+//     ends writes (hit, exact t) to its slot and the lane takes the next ray.
+// Per path, the arithmetic, the draw order and the sample record are the
+// chunked kernel's (the same path_begin / path_pre / path_post, the same walk),
+// so the image is bit-identical; the accumulate pass is unchanged.
+// ---------------------------------------------------------------------------
+struct WfState {
+    float4* s0;            // {o, d.x}
+    float4* s1;            // {d.y, d.z, T.x, T.y}
+    float4* s2;            // {T.z, rng lo, rng hi, -}
+    int4* s3;              // {pass slot, s, s_end, phase}: phase = bounces (a ray in flight), PH_NEW, PH_ITEM
+    float4* hit;           // {t lo, t hi, prim + 1, -} (t: the Real's bits)
+    uint8_t* flag;         // 1: the slot's ray is to be traced this iteration
+    int2* wpool;           // per shade wave: its item range {pool_next, pool_end}; pool_next = INT_MAX: exhausted
+    unsigned int* traced;  // per iteration: 1 when the trace kernel walked any ray
+    int32_t n;             // slots
+    int32_t per_wave;      // trace kernel: slots per wave (a multiple of 64)
+};
+constexpr int kBlockWf = 256;
+#ifndef RT_WF_WAVES
+#define RT_WF_WAVES 5  // trace kernel: waves per SIMD (launch bound: <= 96 VGPRs)
+#endif
+constexpr int kWfWavesPerSimd = RT_WF_WAVES;
+
+template <class Real>  // (a template: the header is in several units)
+__global__ __launch_bounds__(kBlockWf) void wf_init_kernel(WfState W, SampleBuf sb) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < W.n) {
+        W.s3[p] = make_int4(0, 0, 0, PH_ITEM);
+        W.flag[p] = 0;
+    }
+    const int w = p;  // shade wave w's static first pool (first_pool, per shade wave)
+    if (w < (W.n + kWave - 1) / kWave) {
+        const long a = (long)w * sb.pool;
+        W.wpool[w] = a < sb.n_items ? make_int2((int)a, (int)min(a + sb.pool, (long)sb.n_items))
+                                    : make_int2(0x7fffffff, 0x7fffffff);
+    }
+}
+
+template <class Real>
+__global__ __launch_bounds__(kBlockWf) void wf_shade_kernel(DevScene S, RtRegion reg, RenderOut out, int tiles_x,
+                                                            SampleBuf sb, WfState W, int it) {
+    if (it > 0 && W.traced[it - 1] == 0u) return;  // the pass ended an iteration ago
+    __shared__ PhaseRow ptab[kMaxPhases];
+    phase_table_init(sb, ptab);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int wave = p / kWave;
+    const bool valid = p < W.n;
+    const RtCamera& C0 = S.cam;
+    const int endX = min(reg.x + reg.width, C0.width);
+    const int endY = min(reg.y + reg.height, C0.height);
+    const double rtx = 1.0 / (double)tiles_x;
+    unsigned long long st_err = 0;
+    Prof pf;
+    int4 q = valid ? W.s3[p] : make_int4(0, 0, 0, PH_ITEM);
+    int slot = q.x, s = q.y, s_end = q.z, phase = q.w;
+    Path<false> P;
+    P.em_n = 0;
+    bool ray = false;
+    auto record = [&](V3 c) {
+        float4 r;
+        r.x = c.x;
+        r.y = c.y;
+        r.z = c.z;
+        r.w = __int_as_float(P.bounces);
+        rec_store<false>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
+        ++s;
+        phase = s < s_end ? PH_NEW : PH_ITEM;
+    };
+    const RtCamera& C = cam_opaque();
+    if (valid && phase >= 0) {  // the ray traced last iteration: the rest of its level
+        const float4 a = W.s0[p], b = W.s1[p], c2 = W.s2[p], h = W.hit[p];
+        P.o = V3{a.x, a.y, a.z};
+        P.d = V3{a.w, b.x, b.y};
+        P.T = V3{b.z, b.w, c2.x};
+        P.rng = (uint64_t)__float_as_uint(c2.y) | ((uint64_t)__float_as_uint(c2.z) << 32);
+        P.bounces = phase;
+        Real t;
+        if (sizeof(Real) == 8)
+            t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(h.x) |
+                                                       ((unsigned long long)__float_as_uint(h.y) << 32)));
+        else
+            t = (Real)h.x;
+        V3 c;
+        if (path_post<Real, false, false, false>(S, C, P, __float_as_int(h.z) - 1, t, nullptr, st_err, pf, c)) record(c);
+        else if (path_pre<Real, false, false>(C, P, pf, c)) record(c);
+        else ray = true;
+    }
+    // item hand-out (the chunked kernel's guided schedule, per shade wave) and path starts,
+    // until every lane has a ray or no work is left
+    int2 wp = W.wpool[min(wave, (W.n - 1) / kWave)];
+    int pool_next = __builtin_amdgcn_readfirstlane(wp.x), pool_end = __builtin_amdgcn_readfirstlane(wp.y);
+    bool exhausted = pool_next == 0x7fffffff;
+    while (true) {
+        const unsigned long long need = __ballot(valid && !ray && phase == PH_ITEM);
+        if (need != 0ull && !exhausted) {
+            if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
+            if (!exhausted) {
+                const int take = min(__popcll(need), pool_end - pool_next);
+                const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                if (valid && !ray && phase == PH_ITEM && rank < take) {
+                    int tl, l, s1, e1, i, j;
+                    item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
+                    if (slot_pixel(sb, reg, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
+                        slot = tl * 64 + l;
+                        s = s1;
+                        s_end = e1;
+                        phase = PH_NEW;
+                    }
+                }
+                pool_next += take;
+            }
+        }
+        const bool start = valid && !ray && phase == PH_NEW;
+        if (__ballot(start) == 0ull) {
+            if (need == 0ull || exhausted) break;
+            continue;  // items consumed without a pixel (outside the region): hand out more
+        }
+        if (start) {
+            int i, j;
+            slot_pixel(sb, reg, tiles_x, rtx, endX, endY, slot, i, j);
+            path_begin<Real, false>(C, P, pixel_center<Real>(C, i, j), (uint32_t)j * (uint32_t)C.width + (uint32_t)i,
+                                    (uint32_t)(sb.s_base + s));
+            V3 c;
+            if (path_pre<Real, false, false>(C, P, pf, c)) record(c);
+            else ray = true;
+        }
+    }
+    if (valid) {
+        if (ray) {
+            phase = P.bounces;
+            W.s0[p] = make_float4(P.o.x, P.o.y, P.o.z, P.d.x);
+            W.s1[p] = make_float4(P.d.y, P.d.z, P.T.x, P.T.y);
+            W.s2[p] = make_float4(P.T.z, __uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)), 0.f);
+        }
+        W.s3[p] = make_int4(slot, s, s_end, phase);
+        W.flag[p] = ray ? 1 : 0;
+        if (lane == 0) W.wpool[wave] = make_int2(exhausted ? 0x7fffffff : pool_next, exhausted ? 0x7fffffff : pool_end);
+    }
+    const unsigned long long err = wave_or(st_err);
+    if (lane == 0 && err) atomicOr(&out.stats[ST_ERROR * kStatStride], err);
+}
+
+template <class Real, int TRAV>
+__global__ __launch_bounds__(kBlockWf, kWfWavesPerSimd) void wf_trace_kernel(DevScene S, WfState W, SampleBuf sb,
+                                                                              int it) {
+    if (it > 0 && W.traced[it - 1] == 0u) return;
+    extern __shared__ int lds_stack[];
+    __shared__ int xfer[kBlockWf / kWave][kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    int* stk = lds_stack + threadIdx.x;  // this lane's stack column (stride kBlockWf)
+    const int gw = blockIdx.x * (kBlockWf / kWave) + wv;
+    const long b0 = (long)gw * W.per_wave;
+    const int end = (int)min(b0 + W.per_wave, (long)W.n);
+    int next = (int)min(b0, (long)W.n);  // wave-uniform scan position
+    int slot = -1;
+    bool walking = false, any = false;
+    FastWalk<Real> Wk;
+    V3 o = v3(0, 0, 0), d = o;
+    while (true) {
+        // idle lanes take the next flagged slots of the wave's run, in slot order
+        while (next < end) {
+            const unsigned long long idle = __ballot(slot < 0);
+            const int n_idle = __popcll(idle);
+            if (n_idle == 0 || (n_idle < sb.refill_min && __ballot(walking) != 0ull)) break;
+            const int qs = next + lane;
+            const bool act = qs < end && W.flag[qs] != 0;
+            const unsigned long long m = __ballot(act);
+            const int n_act = __popcll(m);
+            const int take = min(n_act, n_idle);
+            const int ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (act && ra < take) xfer[wv][ra] = qs;
+            // the scan resumes after the last slot taken (all 64 when every flagged one was)
+            int last = next + kWave - 1;
+            if (take < n_act) {
+                const unsigned long long lastm = __ballot(act && ra == take - 1);
+                last = take > 0 ? next + (63 - __builtin_clzll(lastm)) : next - 1;
+            }
+            next = min(last + 1, end);
+            __asm__ volatile("" ::: "memory");  // the xfer writes before the reads (one wave: LDS in order)
+            const int ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            if (slot < 0 && ri < take) {
+                slot = xfer[wv][ri];
+                const float4 a = W.s0[slot], b = W.s1[slot];
+                o = V3{a.x, a.y, a.z};
+                d = V3{a.w, b.x, b.y};
+                fast_walk_begin<Real, false>(S, o, d, Wk, nullptr);
+                walking = true;
+                any = true;
+            }
+            __asm__ volatile("" ::: "memory");
+            if (take == 0 && next >= end) break;
+        }
+        if (__ballot(walking) == 0ull && next >= end) break;
+        fast_walk_rounds<Real, false, TRAV == TRAV_FAST_DEFER, false, kBlockWf>(S, o, d, Wk, walking, stk,
+                                                                               sb.min_ready, next >= end, nullptr);
+        if (slot >= 0 && !walking) {
+            fast_walk_resolve<Real, false>(S, o, d, Wk, nullptr);
+            float tx, ty;
+            if (sizeof(Real) == 8) {
+                const unsigned long long tb = (unsigned long long)__double_as_longlong((double)Wk.best_t);
+                tx = __uint_as_float((uint32_t)tb);
+                ty = __uint_as_float((uint32_t)(tb >> 32));
+            } else {
+                tx = (float)Wk.best_t;
+                ty = 0.f;
+            }
+            W.hit[slot] = make_float4(tx, ty, __int_as_float(Wk.best + 1), 0.f);
+            slot = -1;
+        }
+    }
+    if (__ballot(any) != 0ull && lane == 0) W.traced[it] = 1u;
+}
+
 }  // namespace rt

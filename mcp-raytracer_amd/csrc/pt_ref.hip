@@ -277,6 +277,28 @@ hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut&
     return hipGetLastError();
 }
 
+// Wavefront passes (pt_kernel.hpp WfState): init, then per iteration shade + trace.
+hipError_t launch_wf_init(const WfState& W, const SampleBuf& sb, hipStream_t stream) {
+    const int n = std::max(W.n, (W.n + kWave - 1) / kWave);
+    hipLaunchKernelGGL(wf_init_kernel<double>, dim3((n + kBlockWf - 1) / kBlockWf), dim3(kBlockWf), 0, stream, W, sb);
+    return hipGetLastError();
+}
+hipError_t launch_wf_iteration(bool defer, const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
+                               const SampleBuf& sb, const WfState& W, int it, int trace_grid, size_t trace_lds,
+                               hipStream_t stream) {
+    hipLaunchKernelGGL(wf_shade_kernel<double>, dim3((W.n + kBlockWf - 1) / kBlockWf), dim3(kBlockWf), 0, stream, S,
+                       reg, out, tiles_x, sb, W, it);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (defer)
+        hipLaunchKernelGGL((wf_trace_kernel<double, TRAV_FAST_DEFER>), dim3(trace_grid), dim3(kBlockWf), trace_lds,
+                           stream, S, W, sb, it);
+    else
+        hipLaunchKernelGGL((wf_trace_kernel<double, TRAV_FAST>), dim3(trace_grid), dim3(kBlockWf), trace_lds, stream,
+                           S, W, sb, it);
+    return hipGetLastError();
+}
+
 hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* counters, unsigned int* tile_counter,
                              hipStream_t stream) {
     hipLaunchKernelGGL(init_stats_kernel, dim3(1), dim3(64), 0, stream, stats, counters, tile_counter);

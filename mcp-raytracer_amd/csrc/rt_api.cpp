@@ -155,6 +155,7 @@ struct rt_camera {
         sbuf_cap = 0;
         d_wslots = nullptr;
         wslots_cap = 0;
+        free_wf();
         free_adapt_buffers();
         if (d_acount) (void)hipFree(d_acount);
         d_acount = nullptr;
@@ -533,6 +534,90 @@ struct rt_camera {
             hip_check(e, "pt_chunk_kernel launch");
             hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
         };
+        // Wavefront passes (wf_shade_kernel / wf_trace_kernel): fixed-spp ref-precision launches of
+        // trees walked from global memory with at least 2^26 samples (RT_AMD_WAVEFRONT=1 forces them
+        // for any fast-traversal scene, 0 keeps the chunked kernel).
+        const int wf_env = env_int("RT_AMD_WAVEFRONT", -1);
+        const bool wf_ok = !rounds && prec == PREC_REF && !v.emit && count == 0 && trav_fast(v.trav);
+        const bool wf = wf_ok && (wf_env == 1 || (wf_env < 0 && g.lds_level == 0 &&
+                                                  (double)mine * kWave * (double)C.n_samples >= (double)(1 << 26)));
+        auto run_pass_wf = [&](bool first) {
+            // the guided schedule over P slots: first items of pow2floor(spl / 4) <= 8 samples
+            // (spl: samples per slot), takes of 4 tile-chunks
+            const long pass_samples = (long)sb.slots * C.n_samples;
+            const long P = std::max<long>(256, std::min<long>((long)env_int("RT_AMD_WF_SLOTS", 8 << 20),
+                                                              (pass_samples / 8 + 255) / 256 * 256));
+            const double spl = (double)pass_samples / (double)P;
+            int c = 1;
+            while (c * 2 <= std::min(8.0, spl / 4.0)) c *= 2;
+            c = std::min(c, std::max(1, C.n_samples / 2));
+            int s0 = 0, np = 0;
+            while (s0 < C.n_samples) {
+                const int rem = C.n_samples - s0;
+                if (c <= 1 || np == kMaxPhases - 1) {
+                    sb.s0[np] = s0; sb.chunk[np] = 1; sb.nch[np] = rem; ++np;
+                    break;
+                }
+                const int span = (rem / 2) / c * c;
+                if (span == 0) { c /= 2; continue; }
+                sb.s0[np] = s0; sb.chunk[np] = c; sb.nch[np] = span / c; ++np;
+                s0 += span;
+                c /= 2;
+            }
+            sb.n_phases = np;
+            for (int q = 0; q < np; ++q) sb.rnch[q] = 1.0 / (double)sb.nch[q];
+            sb.pool = kWave * std::max(1, env_int("RT_AMD_WF_POOL", 4));
+            sb.refill_min = std::min(env_int("RT_AMD_WF_REFILL", 4), kWave);
+            sb.min_ready = std::min(env_int("RT_AMD_WF_READY", 8), kWave);
+            const long group_slots = ((long)sb.slots + kWave - 1) / kWave * kWave;
+            long items = 0;
+            for (int q = 0; q < np; ++q) {
+                sb.item_base[q] = (int32_t)items;
+                items += group_slots * sb.nch[q];
+            }
+            if (items >= (1l << 31) - (1l << 24)) throw std::runtime_error("wavefront pass too large");
+            sb.n_items = (int32_t)items;
+            const long gwaves = P / kWave;
+            const long static_end = std::min<long>(gwaves * sb.pool, items);
+            const long tail_items = (long)std::max(env_int("RT_AMD_TAIL", 4), 0) * gwaves * sb.pool / 4;
+            sb.tail_from = (int32_t)std::min<long>(items, std::max<long>(static_end, items - tail_items));
+            sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 2));
+            if (!first) hip_check(hipMemsetAsync(d_tile, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");
+            ensure_wf((size_t)P);
+            WfState W{};
+            W.s0 = d_wf_s[0];
+            W.s1 = d_wf_s[1];
+            W.s2 = d_wf_s[2];
+            W.s3 = reinterpret_cast<int4*>(d_wf_s[3]);
+            W.hit = d_wf_s[4];
+            W.flag = d_wf_flag;
+            W.wpool = d_wf_pool;
+            W.traced = d_wf_traced;
+            W.n = (int32_t)P;
+            const int trace_grid = std::max(1, cus * kWfWavesPerSimd);
+            const long trace_waves = (long)trace_grid * (kBlockWf / kWave);
+            W.per_wave = (int32_t)(((P + trace_waves - 1) / trace_waves + kWave - 1) / kWave * kWave);
+            const size_t trace_lds = (size_t)std::max(C.stack_depth, 1) * kBlockWf * sizeof(int);
+            hip_check(hipEventRecord(pass_event(pass, 0), stream), "hipEventRecord");
+            hip_check(hipMemsetAsync(d_wf_traced, 0, kWfMaxIter * sizeof(unsigned int), stream), "hipMemsetAsync");
+            hip_check(launch_wf_init(W, sb, stream), "wf_init_kernel launch");
+            constexpr int kBatch = 32;
+            for (int it = 0;; it += kBatch) {
+                if (it + kBatch > kWfMaxIter) throw std::runtime_error("wavefront pass: too many iterations");
+                for (int k = it; k < it + kBatch; ++k)
+                    hip_check(launch_wf_iteration(v.defer, S, reg, out, g.tiles_x, sb, W, k, trace_grid, trace_lds,
+                                                  stream),
+                              "wf_shade / wf_trace launch");
+                hip_check(hipMemcpyAsync(h_wf_traced, d_wf_traced + it, kBatch * sizeof(unsigned int),
+                                         hipMemcpyDeviceToHost, stream),
+                          "hipMemcpyAsync");
+                hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+                bool done = false;
+                for (int k = 0; k < kBatch; ++k) done = done || h_wf_traced[k] == 0u;
+                if (done) break;
+            }
+            hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
+        };
         if (rounds) {
             launch_adaptive_rounds(S, reg, out, g, mine, sb, schedule, run_pass, pass, stream);
         } else {
@@ -554,14 +639,15 @@ struct rt_camera {
                     sb.stride_s = sb.slots;
                     sb.stride_slot = 1;
                 }
-                run_pass(t0 == 0);
+                if (wf) run_pass_wf(t0 == 0);
+                else run_pass(t0 == 0);
                 hip_check(launch_accum(S, reg, out, g.tiles_x, sb, stream), "pt_accum_kernel launch");
                 hip_check(hipEventRecord(pass_event(pass, 2), stream), "hipEventRecord");
             }
         }
         n_passes = pass;
         ev_accum = true;
-        last_kernel = v.wpool ? RT_KERNEL_WPOOL : v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
+        last_kernel = wf ? RT_KERNEL_WAVEFRONT : v.wpool ? RT_KERNEL_WPOOL : v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
     }
 
     // Adaptive sampling in rounds (src/camera.ts:400-425). Round r renders samples
@@ -660,6 +746,38 @@ struct rt_camera {
     // Per-sample record buffer of the chunked kernel (grown on demand, kept).
     float4* d_sbuf = nullptr;
     size_t sbuf_cap = 0;
+    // wavefront passes: the slots' state (s0, s1, s2, s3, hit: P float4 each), ray flags, the
+    // shade waves' item ranges and the per-iteration "traced" words (+ a pinned host copy)
+    static constexpr int kWfMaxIter = 1 << 20;
+    float4* d_wf_s[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    uint8_t* d_wf_flag = nullptr;
+    int2* d_wf_pool = nullptr;
+    unsigned int* d_wf_traced = nullptr;
+    unsigned int* h_wf_traced = nullptr;
+    size_t wf_cap = 0;
+    void free_wf() {
+        for (float4*& q : d_wf_s)
+            if (q) (void)hipFree(q), q = nullptr;
+        if (d_wf_flag) (void)hipFree(d_wf_flag);
+        if (d_wf_pool) (void)hipFree(d_wf_pool);
+        if (d_wf_traced) (void)hipFree(d_wf_traced);
+        if (h_wf_traced) (void)hipHostFree(h_wf_traced);
+        d_wf_flag = nullptr;
+        d_wf_pool = nullptr;
+        d_wf_traced = nullptr;
+        h_wf_traced = nullptr;
+        wf_cap = 0;
+    }
+    void ensure_wf(size_t n) {
+        if (n <= wf_cap) return;
+        free_wf();
+        for (float4*& q : d_wf_s) hip_check(hipMalloc(&q, n * sizeof(float4)), "hipMalloc(wavefront slots)");
+        hip_check(hipMalloc(&d_wf_flag, n), "hipMalloc(wavefront flags)");
+        hip_check(hipMalloc(&d_wf_pool, (n / kWave + 1) * sizeof(int2)), "hipMalloc(wavefront pools)");
+        hip_check(hipMalloc(&d_wf_traced, kWfMaxIter * sizeof(unsigned int)), "hipMalloc(wavefront flags)");
+        hip_check(hipHostMalloc(&h_wf_traced, 64 * sizeof(unsigned int), hipHostMallocDefault), "hipHostMalloc");
+        wf_cap = n;
+    }
     // walker-pool kernel: the path slots of every resident wave (HBM)
     float4* d_wslots = nullptr;
     size_t wslots_cap = 0;

@@ -989,3 +989,96 @@ def test_wpool_full_size_spheres500_rows_match_oracle(rt, oracle, gpu, monkeypat
     cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
     assert_identical(rad, rgb, rad2, rgb2, "wpool == chunked spheres-500 800^2")
     assert st.bounces == st2.bounces
+
+
+# ---------------------------------------------------------------------------
+# Wavefront passes (wf_shade_kernel / wf_trace_kernel; automatic for large launches of
+# trees walked from global memory, forced here with RT_AMD_WAVEFRONT=1 on small ones).
+# Same records as the chunked kernel: images and stats bit-identical to it and the oracle.
+# ---------------------------------------------------------------------------
+WF_CASES = {
+    "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                {"width": 48, "aspect": 1, "samples": 8, "depth": 8, **NOADAPT}, {}),
+    "rain": ({"type": "rain", "options": {"seed": 42}}, {"width": 64, "samples": 8, "depth": 16, **NOADAPT}, {}),
+    "spheres_deep": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                     {"width": 40, "aspect": 1, "samples": 6, "depth": 120, **NOADAPT}, {}),
+    "spheres_aperture": ({"type": "spheres", "options": {"count": 200, "seed": 7}},
+                         {"width": 40, "aspect": 1.5, "samples": 5, "depth": 10, **NOADAPT}, {}),
+    # few slots: every slot runs many items; several trace waves per slot run
+    "spheres_few_slots": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                          {"width": 40, "aspect": 1, "samples": 9, "depth": 8, **NOADAPT}, {"RT_AMD_WF_SLOTS": "256"}),
+    # several record passes (1 MB budget)
+    "spheres_multipass": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
+                          {"width": 64, "aspect": 1, "samples": 12, "depth": 8, **NOADAPT}, {"RT_AMD_SBUF_MB": "1"}),
+    "spheres2k_deferred": ({"type": "spheres", "options": {"count": 2000, "seed": 5}},
+                           {"width": 40, "aspect": 1, "samples": 6, "depth": 12, **NOADAPT}, {"RT_AMD_DEFER": "1"}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(WF_CASES))
+def test_wavefront_matches_oracle_and_chunked(rt, oracle, gpu, case, monkeypatch):
+    cfg, ro, env = WF_CASES[case]
+    sd = rt.generate_scene_data(cfg)
+    if case == "spheres_aperture":
+        sd["camera"]["aperture"] = 0.1
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == "wavefront"
+    if case == "spheres_multipass":
+        assert cam.pass_count() > 1
+    orc = oracle.render(sd, ro)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wavefront {case}")
+    assert_stats_identical(st, orc["stats"])
+    monkeypatch.setenv("RT_AMD_WAVEFRONT", "0")
+    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
+    assert cam2.last_kernel() == "chunked"
+    assert_identical(rad, rgb, rad2, rgb2, f"wavefront == chunked {case}")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_wavefront_random_scenes_match_oracle(rt, oracle, gpu, seed, monkeypatch):
+    sd = _random_scene(seed)
+    ro = {"width": 32, "samples": 4, "depth": 8, **NOADAPT, "traversal": "fast"}
+    orc = oracle.render(sd, ro)
+    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wavefront random {seed} ({cam.last_kernel()})")
+    assert_stats_identical(st, orc["stats"])
+
+
+def test_wavefront_regions_and_tile_groups(rt, oracle, gpu, monkeypatch):
+    """A region smaller than a tile and an 8-way tile split through the wavefront path."""
+    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 500, "seed": 42}})
+    ro = {"width": 40, "aspect": 1, "samples": 7, "depth": 8, **NOADAPT}
+    orc = oracle.render(sd, ro)
+    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
+    cam = rt.create_camera_from_scene_data(sd, ro)
+    rgb2 = np.zeros_like(orc["rgb"])
+    rad2 = np.zeros_like(orc["radiance"])
+    cam.render_region(rgb2, (17, 11, 3, 5), radiance=rad2)
+    assert cam.last_kernel() == "wavefront"
+    assert_identical(rad2[11:16, 17:20], rgb2[11:16, 17:20], orc["radiance"][11:16, 17:20], orc["rgb"][11:16, 17:20],
+                     "wavefront 3x5 region")
+    assert not rgb2[:11].any() and not rgb2[16:].any()
+    import torch
+    H, W = orc["rgb"].shape[:2]
+    frame = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    for g in range(8):
+        cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=g, tile_groups=8, synchronize=True)
+    assert np.array_equal(frame.cpu().numpy(), orc["rgb"])
+
+
+def test_wavefront_is_the_default_for_large_global_tree_launches(rt, oracle, gpu):
+    """spheres-100k 2048x2048 spp 16 (2^26 samples, tree in global memory) takes the
+    wavefront path by default; oracle row segments exact."""
+    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 100000, "seed": 42}})
+    ro = {"width": 2048, "aspect": 1, "samples": 16, "depth": 100, **NOADAPT}
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.last_kernel() == "wavefront"
+    assert st.samples["total"] == 2048 * 2048 * 16
+    for (x, y) in [(1022, 950), (500, 1500), (1500, 300)]:
+        orc = oracle.render(sd, ro, region=(x, y, 16, 1), threads=16)
+        assert_identical(rad[y:y + 1, x:x + 16], rgb[y:y + 1, x:x + 16], orc["radiance"][y:y + 1, x:x + 16],
+                         orc["rgb"][y:y + 1, x:x + 16], f"spheres-100k 2048^2 row {y} x {x}")
