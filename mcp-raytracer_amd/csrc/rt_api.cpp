@@ -48,6 +48,11 @@ int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return (e && e[0]) ? std::max(1, std::atoi(e)) : dflt;
 }
+// the same without the clamp to >= 1 (switches and counts where 0 means off)
+int env_int0(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return (e && e[0]) ? std::atoi(e) : dflt;
+}
 
 int set_error(int code, const std::string& msg) {
     g_error = msg;
@@ -490,7 +495,7 @@ struct rt_camera {
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int(v.wpool ? "RT_AMD_WREADY" : "RT_AMD_READY", v.wpool ? 16 : 48), kWave);
-            sb.wpolicy = env_int("RT_AMD_WPOLICY", 0);  // policy 1 measured within noise (profiles/r03/wpool_hbm/)
+            sb.wpolicy = env_int0("RT_AMD_WPOLICY", 0);  // policy 1 measured within noise (profiles/r03/wpool_hbm/)
         };
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
@@ -510,15 +515,13 @@ struct rt_camera {
             LaunchGeom gp = v.wpool ? gw : g;
             const int block = v.wpool ? kBlockWPool : v.pool ? kBlockPool : kBlockChunk;
             gp.grid = (int)std::max<long>(1, std::min<long>(items / block + 1, (long)cus));
-            // the launch's last items - RT_AMD_TAIL quarter-rounds of takes, one round = every
-            // resident wave taking sb.pool items - come in takes of RT_AMD_TAIL_POOL tile-chunks
-            // from a second counter: the waves that draw the last items hold fewer of them.
-            // One round in 2-tile-chunk takes: Cornell rank shares N=1 15.38 -> 15.20 ms, N=8
-            // 2.27 -> 2.20; spheres-500 N=8 1.136 -> 1.089 ms (1-tile-chunk takes: no change,
-            // two rounds: slower; profiles/r03/tail/)
+            // optional tail hand-out: the launch's last items - RT_AMD_TAIL quarter-rounds of takes,
+            // one round = every resident wave taking sb.pool items - in takes of RT_AMD_TAIL_POOL
+            // tile-chunks from a second counter. Off: against a true baseline every setting
+            // measured within noise (Cornell / spheres-500 rank shares, profiles/r03/tail/)
             const long gwaves = (long)gp.grid * (block / kWave);
             const long static_end = std::min<long>(gwaves * sb.pool, items);
-            const long tail_items = (long)std::max(env_int("RT_AMD_TAIL", 4), 0) * gwaves * sb.pool / 4;
+            const long tail_items = (long)std::max(env_int0("RT_AMD_TAIL", 0), 0) * gwaves * sb.pool / 4;
             sb.tail_from = (int32_t)std::min<long>(items, std::max<long>(static_end, items - tail_items));
             sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 2));
             DevScene Sp = S;
@@ -537,7 +540,7 @@ struct rt_camera {
         // Wavefront passes (wf_shade_kernel / wf_trace_kernel): fixed-spp ref-precision launches of
         // trees walked from global memory with at least 2^26 samples (RT_AMD_WAVEFRONT=1 forces them
         // for any fast-traversal scene, 0 keeps the chunked kernel).
-        const int wf_env = env_int("RT_AMD_WAVEFRONT", -1);
+        const int wf_env = env_int0("RT_AMD_WAVEFRONT", -1);
         const bool wf_ok = !rounds && prec == PREC_REF && !v.emit && count == 0 && trav_fast(v.trav);
         const bool wf = wf_ok && (wf_env == 1 || (wf_env < 0 && g.lds_level == 0 &&
                                                   (double)mine * kWave * (double)C.n_samples >= (double)(1 << 26)));
@@ -579,7 +582,7 @@ struct rt_camera {
             sb.n_items = (int32_t)items;
             const long gwaves = P / kWave;
             const long static_end = std::min<long>(gwaves * sb.pool, items);
-            const long tail_items = (long)std::max(env_int("RT_AMD_TAIL", 4), 0) * gwaves * sb.pool / 4;
+            const long tail_items = (long)std::max(env_int0("RT_AMD_TAIL", 0), 0) * gwaves * sb.pool / 4;
             sb.tail_from = (int32_t)std::min<long>(items, std::max<long>(static_end, items - tail_items));
             sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 2));
             if (!first) hip_check(hipMemsetAsync(d_tile, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");

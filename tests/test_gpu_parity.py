@@ -1008,8 +1008,8 @@ WF_CASES = {
     "spheres_few_slots": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
                           {"width": 40, "aspect": 1, "samples": 9, "depth": 8, **NOADAPT}, {"RT_AMD_WF_SLOTS": "256"}),
     # several record passes (1 MB budget)
-    "spheres_multipass": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
-                          {"width": 64, "aspect": 1, "samples": 12, "depth": 8, **NOADAPT}, {"RT_AMD_SBUF_MB": "1"}),
+    "spheres_multipass": ({"type": "spheres", "options": {"count": 500, "seed": 42}},  # 96^2 x 16 x 16 B: 3 passes
+                          {"width": 96, "aspect": 1, "samples": 16, "depth": 8, **NOADAPT}, {"RT_AMD_SBUF_MB": "1"}),
     "spheres2k_deferred": ({"type": "spheres", "options": {"count": 2000, "seed": 5}},
                            {"width": 40, "aspect": 1, "samples": 6, "depth": 12, **NOADAPT}, {"RT_AMD_DEFER": "1"}),
 }
