@@ -3143,10 +3143,27 @@ struct WfState {
     uint8_t* flag;         // 1: the slot's ray is to be traced this iteration
     int2* wpool;           // per shade wave: its item range {pool_next, pool_end}; pool_next = INT_MAX: exhausted
     unsigned int* traced;  // per iteration: 1 when the trace kernel walked any ray
+    unsigned long long* live;  // per shade wave: its slots with a ray in flight (ballot); 0 + exhausted: skip
     int32_t n;             // slots
     int32_t per_wave;      // trace kernel: slots per wave (a multiple of 64)
 };
 constexpr int kBlockWf = 256;
+// The path state streams through HBM once per iteration: non-temporal loads and stores,
+// so it does not evict the BVH (the walk's working set) from the L2 between iterations.
+__device__ __forceinline__ float4 nt_ld(const float4* p) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int4 nt_ld(const int4* p) {
+    const float4 v = nt_ld(reinterpret_cast<const float4*>(p));
+    return make_int4(__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w));
+}
+__device__ __forceinline__ void nt_st(float4* p, float4 v) { rec_store<true>(p, v); }
+__device__ __forceinline__ void nt_st(int4* p, int4 v) {
+    rec_store<true>(reinterpret_cast<float4*>(p),
+                    make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w)));
+}
 #ifndef RT_WF_WAVES
 #define RT_WF_WAVES 5  // trace kernel: waves per SIMD (launch bound: <= 96 VGPRs)
 #endif
@@ -3159,6 +3176,7 @@ __global__ __launch_bounds__(kBlockWf) void wf_init_kernel(WfState W, SampleBuf 
         W.s3[p] = make_int4(0, 0, 0, PH_ITEM);
         W.flag[p] = 0;
     }
+    if (p < (W.n + kWave - 1) / kWave) W.live[p] = 0ull;
     const int w = p;  // shade wave w's static first pool (first_pool, per shade wave)
     if (w < (W.n + kWave - 1) / kWave) {
         const long a = (long)w * sb.pool;
@@ -3177,13 +3195,15 @@ __global__ __launch_bounds__(kBlockWf) void wf_shade_kernel(DevScene S, RtRegion
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const int wave = p / kWave;
     const bool valid = p < W.n;
+    // a wave whose slots are all idle once the items are exhausted is done for the pass
+    if (valid && W.live[wave] == 0ull && W.wpool[wave].x == 0x7fffffff) return;
     const RtCamera& C0 = S.cam;
     const int endX = min(reg.x + reg.width, C0.width);
     const int endY = min(reg.y + reg.height, C0.height);
     const double rtx = 1.0 / (double)tiles_x;
     unsigned long long st_err = 0;
     Prof pf;
-    int4 q = valid ? W.s3[p] : make_int4(0, 0, 0, PH_ITEM);
+    int4 q = valid ? nt_ld(W.s3 + p) : make_int4(0, 0, 0, PH_ITEM);
     int slot = q.x, s = q.y, s_end = q.z, phase = q.w;
     Path<false> P;
     P.em_n = 0;
@@ -3194,13 +3214,13 @@ __global__ __launch_bounds__(kBlockWf) void wf_shade_kernel(DevScene S, RtRegion
         r.y = c.y;
         r.z = c.z;
         r.w = __int_as_float(P.bounces);
-        rec_store<false>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
+        rec_store<true>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
         ++s;
         phase = s < s_end ? PH_NEW : PH_ITEM;
     };
     const RtCamera& C = cam_opaque();
     if (valid && phase >= 0) {  // the ray traced last iteration: the rest of its level
-        const float4 a = W.s0[p], b = W.s1[p], c2 = W.s2[p], h = W.hit[p];
+        const float4 a = nt_ld(W.s0 + p), b = nt_ld(W.s1 + p), c2 = nt_ld(W.s2 + p), h = nt_ld(W.hit + p);
         P.o = V3{a.x, a.y, a.z};
         P.d = V3{a.w, b.x, b.y};
         P.T = V3{b.z, b.w, c2.x};
@@ -3261,13 +3281,18 @@ __global__ __launch_bounds__(kBlockWf) void wf_shade_kernel(DevScene S, RtRegion
     if (valid) {
         if (ray) {
             phase = P.bounces;
-            W.s0[p] = make_float4(P.o.x, P.o.y, P.o.z, P.d.x);
-            W.s1[p] = make_float4(P.d.y, P.d.z, P.T.x, P.T.y);
-            W.s2[p] = make_float4(P.T.z, __uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)), 0.f);
+            nt_st(W.s0 + p, make_float4(P.o.x, P.o.y, P.o.z, P.d.x));
+            nt_st(W.s1 + p, make_float4(P.d.y, P.d.z, P.T.x, P.T.y));
+            nt_st(W.s2 + p, make_float4(P.T.z, __uint_as_float((uint32_t)P.rng),
+                                        __uint_as_float((uint32_t)(P.rng >> 32)), 0.f));
         }
-        W.s3[p] = make_int4(slot, s, s_end, phase);
+        nt_st(W.s3 + p, make_int4(slot, s, s_end, phase));
         W.flag[p] = ray ? 1 : 0;
-        if (lane == 0) W.wpool[wave] = make_int2(exhausted ? 0x7fffffff : pool_next, exhausted ? 0x7fffffff : pool_end);
+    }
+    const unsigned long long live = __ballot(valid && ray);
+    if (valid && lane == 0) {
+        W.wpool[wave] = make_int2(exhausted ? 0x7fffffff : pool_next, exhausted ? 0x7fffffff : pool_end);
+        W.live[wave] = live;
     }
     const unsigned long long err = wave_or(st_err);
     if (lane == 0 && err) atomicOr(&out.stats[ST_ERROR * kStatStride], err);
@@ -3284,37 +3309,50 @@ __global__ __launch_bounds__(kBlockWf, kWfWavesPerSimd) void wf_trace_kernel(Dev
     int* stk = lds_stack + threadIdx.x;  // this lane's stack column (stride kBlockWf)
     const int gw = blockIdx.x * (kBlockWf / kWave) + wv;
     const long b0 = (long)gw * W.per_wave;
-    const int end = (int)min(b0 + W.per_wave, (long)W.n);
-    int next = (int)min(b0, (long)W.n);  // wave-uniform scan position
+    const int end = (int)min(b0 + W.per_wave, (long)W.n);  // per_wave and n are multiples of 256
+    int win = (int)min(b0, (long)W.n);  // the scan window [win, win + 256): one flag word (4 slots) per lane
+    bool have = win < end;
+    // the window's flagged slots not taken yet, by sub-window q: slot win + 4 * lane + q
+    unsigned long long rem[4] = {0ull, 0ull, 0ull, 0ull};
+    const uint32_t* fw = reinterpret_cast<const uint32_t*>(W.flag);
+    auto load_window = [&]() {
+        const int x = win + 4 * lane;
+        const uint32_t word = x < end ? fw[x >> 2] : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rem[q] = __ballot(((word >> (8 * q)) & 0xffu) != 0u);
+    };
+    if (have) load_window();
     int slot = -1;
     bool walking = false, any = false;
     FastWalk<Real> Wk;
     V3 o = v3(0, 0, 0), d = o;
     while (true) {
-        // idle lanes take the next flagged slots of the wave's run, in slot order
-        while (next < end) {
+        // idle lanes take the window's next flagged slots (ballot ranks through LDS)
+        while (have) {
             const unsigned long long idle = __ballot(slot < 0);
             const int n_idle = __popcll(idle);
             if (n_idle == 0 || (n_idle < sb.refill_min && __ballot(walking) != 0ull)) break;
-            const int qs = next + lane;
-            const bool act = qs < end && W.flag[qs] != 0;
-            const unsigned long long m = __ballot(act);
-            const int n_act = __popcll(m);
-            const int take = min(n_act, n_idle);
-            const int ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (act && ra < take) xfer[wv][ra] = qs;
-            // the scan resumes after the last slot taken (all 64 when every flagged one was)
-            int last = next + kWave - 1;
-            if (take < n_act) {
-                const unsigned long long lastm = __ballot(act && ra == take - 1);
-                last = take > 0 ? next + (63 - __builtin_clzll(lastm)) : next - 1;
+            const int q = rem[0] ? 0 : rem[1] ? 1 : rem[2] ? 2 : rem[3] ? 3 : 4;
+            if (q == 4) {
+                win += 4 * kWave;
+                have = win < end;
+                if (have) load_window();
+                continue;
             }
-            next = min(last + 1, end);
+            const unsigned long long m = rem[0] ? rem[0] : rem[1] ? rem[1] : rem[2] ? rem[2] : rem[3];
+            const bool act = (m >> lane) & 1ull;
+            const int take = min(__popcll(m), n_idle);
+            const int ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (act && ra < take) xfer[wv][ra] = win + 4 * lane + q;
+            const unsigned long long taken = __ballot(act && ra < take);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k == q) rem[k] &= ~taken;
             __asm__ volatile("" ::: "memory");  // the xfer writes before the reads (one wave: LDS in order)
             const int ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (slot < 0 && ri < take) {
                 slot = xfer[wv][ri];
-                const float4 a = W.s0[slot], b = W.s1[slot];
+                const float4 a = nt_ld(W.s0 + slot), b = nt_ld(W.s1 + slot);
                 o = V3{a.x, a.y, a.z};
                 d = V3{a.w, b.x, b.y};
                 fast_walk_begin<Real, false>(S, o, d, Wk, nullptr);
@@ -3322,8 +3360,8 @@ __global__ __launch_bounds__(kBlockWf, kWfWavesPerSimd) void wf_trace_kernel(Dev
                 any = true;
             }
             __asm__ volatile("" ::: "memory");
-            if (take == 0 && next >= end) break;
         }
+        const int next = have ? win : end;  // (scan state for the drain decision below)
         if (__ballot(walking) == 0ull && next >= end) break;
         fast_walk_rounds<Real, false, TRAV == TRAV_FAST_DEFER, false, kBlockWf>(S, o, d, Wk, walking, stk,
                                                                                sb.min_ready, next >= end, nullptr);
@@ -3338,7 +3376,7 @@ __global__ __launch_bounds__(kBlockWf, kWfWavesPerSimd) void wf_trace_kernel(Dev
                 tx = (float)Wk.best_t;
                 ty = 0.f;
             }
-            W.hit[slot] = make_float4(tx, ty, __int_as_float(Wk.best + 1), 0.f);
+            nt_st(W.hit + slot, make_float4(tx, ty, __int_as_float(Wk.best + 1), 0.f));
             slot = -1;
         }
     }

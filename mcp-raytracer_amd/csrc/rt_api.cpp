@@ -537,13 +537,14 @@ struct rt_camera {
             hip_check(e, "pt_chunk_kernel launch");
             hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
         };
-        // Wavefront passes (wf_shade_kernel / wf_trace_kernel): fixed-spp ref-precision launches of
-        // trees walked from global memory with at least 2^26 samples (RT_AMD_WAVEFRONT=1 forces them
-        // for any fast-traversal scene, 0 keeps the chunked kernel).
-        const int wf_env = env_int0("RT_AMD_WAVEFRONT", -1);
-        const bool wf_ok = !rounds && prec == PREC_REF && !v.emit && count == 0 && trav_fast(v.trav);
-        const bool wf = wf_ok && (wf_env == 1 || (wf_env < 0 && g.lds_level == 0 &&
-                                                  (double)mine * kWave * (double)C.n_samples >= (double)(1 << 26)));
+        // Wavefront passes (wf_shade_kernel / wf_trace_kernel), opt-in (RT_AMD_WAVEFRONT=1) for
+        // fixed-spp ref-precision fast-traversal launches: bit-identical, but on spheres-100k 2048^2
+        // spp16 92 ms against the chunked kernel's 40 ms - the walk-only kernel runs the same
+        // instructions per ray on more lanes (0.45 vs 0.36) yet each of the ~160 iterations ends on
+        // a device-wide drain of its walks, and the path state streams through HBM twice per
+        // iteration (profiles/r03/wavefront/).
+        const bool wf = !rounds && prec == PREC_REF && !v.emit && count == 0 && trav_fast(v.trav) &&
+                        env_int0("RT_AMD_WAVEFRONT", 0) == 1;
         auto run_pass_wf = [&](bool first) {
             // the guided schedule over P slots: first items of pow2floor(spl / 4) <= 8 samples
             // (spl: samples per slot), takes of 4 tile-chunks
@@ -596,11 +597,19 @@ struct rt_camera {
             W.flag = d_wf_flag;
             W.wpool = d_wf_pool;
             W.traced = d_wf_traced;
+            W.live = d_wf_live;
             W.n = (int32_t)P;
-            const int trace_grid = std::max(1, cus * kWfWavesPerSimd);
-            const long trace_waves = (long)trace_grid * (kBlockWf / kWave);
-            W.per_wave = (int32_t)(((P + trace_waves - 1) / trace_waves + kWave - 1) / kWave * kWave);
+            // one resident wave per SIMD per block: as many blocks per CU as the VGPR bound
+            // (kWfWavesPerSimd) and the walkers' LDS stacks allow - every block resident at once,
+            // since each owns a fixed run of slots (a second round of blocks doubled the time)
             const size_t trace_lds = (size_t)std::max(C.stack_depth, 1) * kBlockWf * sizeof(int);
+            const int per_cu = std::max(1, std::min<int>(kWfWavesPerSimd, (int)((size_t)lds_max / (trace_lds + 1024))));
+            const int trace_grid = std::max(1, cus * per_cu);
+            const long trace_waves = (long)trace_grid * (kBlockWf / kWave);
+            W.per_wave = (int32_t)(((P + trace_waves - 1) / trace_waves + 255) / 256 * 256);  // whole flag words
+            if (env_flag("RT_AMD_LAUNCH_LOG", false))
+                std::fprintf(stderr, "[rt wavefront] slots %ld stack_depth %d trace blocks/CU %d grid %d slots/wave %d\n",
+                             P, C.stack_depth, per_cu, trace_grid, W.per_wave);
             hip_check(hipEventRecord(pass_event(pass, 0), stream), "hipEventRecord");
             hip_check(hipMemsetAsync(d_wf_traced, 0, kWfMaxIter * sizeof(unsigned int), stream), "hipMemsetAsync");
             hip_check(launch_wf_init(W, sb, stream), "wf_init_kernel launch");
@@ -755,6 +764,7 @@ struct rt_camera {
     float4* d_wf_s[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     uint8_t* d_wf_flag = nullptr;
     int2* d_wf_pool = nullptr;
+    unsigned long long* d_wf_live = nullptr;
     unsigned int* d_wf_traced = nullptr;
     unsigned int* h_wf_traced = nullptr;
     size_t wf_cap = 0;
@@ -763,10 +773,12 @@ struct rt_camera {
             if (q) (void)hipFree(q), q = nullptr;
         if (d_wf_flag) (void)hipFree(d_wf_flag);
         if (d_wf_pool) (void)hipFree(d_wf_pool);
+        if (d_wf_live) (void)hipFree(d_wf_live);
         if (d_wf_traced) (void)hipFree(d_wf_traced);
         if (h_wf_traced) (void)hipHostFree(h_wf_traced);
         d_wf_flag = nullptr;
         d_wf_pool = nullptr;
+        d_wf_live = nullptr;
         d_wf_traced = nullptr;
         h_wf_traced = nullptr;
         wf_cap = 0;
@@ -777,6 +789,7 @@ struct rt_camera {
         for (float4*& q : d_wf_s) hip_check(hipMalloc(&q, n * sizeof(float4)), "hipMalloc(wavefront slots)");
         hip_check(hipMalloc(&d_wf_flag, n), "hipMalloc(wavefront flags)");
         hip_check(hipMalloc(&d_wf_pool, (n / kWave + 1) * sizeof(int2)), "hipMalloc(wavefront pools)");
+        hip_check(hipMalloc(&d_wf_live, (n / kWave + 1) * sizeof(unsigned long long)), "hipMalloc(wavefront masks)");
         hip_check(hipMalloc(&d_wf_traced, kWfMaxIter * sizeof(unsigned int)), "hipMalloc(wavefront flags)");
         hip_check(hipHostMalloc(&h_wf_traced, 64 * sizeof(unsigned int), hipHostMallocDefault), "hipHostMalloc");
         wf_cap = n;

@@ -1070,11 +1070,12 @@ def test_wavefront_regions_and_tile_groups(rt, oracle, gpu, monkeypatch):
     assert np.array_equal(frame.cpu().numpy(), orc["rgb"])
 
 
-def test_wavefront_is_the_default_for_large_global_tree_launches(rt, oracle, gpu):
-    """spheres-100k 2048x2048 spp 16 (2^26 samples, tree in global memory) takes the
-    wavefront path by default; oracle row segments exact."""
+def test_wavefront_spheres100k_2048_rows_match_oracle(rt, oracle, gpu, monkeypatch):
+    """spheres-100k 2048x2048 spp 16 (2^26 samples, tree in global memory) through the
+    wavefront passes: oracle row segments exact."""
     sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 100000, "seed": 42}})
     ro = {"width": 2048, "aspect": 1, "samples": 16, "depth": 100, **NOADAPT}
+    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
     cam, rgb, rad, st = _render_gpu(rt, sd, ro)
     assert cam.last_kernel() == "wavefront"
     assert st.samples["total"] == 2048 * 2048 * 16
