@@ -2164,8 +2164,6 @@ struct SampleBuf {
     int32_t n_items;
     int32_t refill_min;  // idle lanes that trigger a hand-out (all-idle always does)
     int32_t min_ready;   // resumable fast traversal: lanes done walking before the wave shades
-    int32_t tail_from, tail_pool;  // the launch's last items [tail_from, n_items): takes of tail_pool items
-    int32_t wpolicy;     // walker-pool kernel: stage policy (0: full trips first, 1: shade when walkers starve)
     // Adaptive-sampling rounds (pt_adapt_kernel): the pass's record slot a renders the launch
     // slot act[a] (tile * 64 + lane over the launch's tiles; tile0 is 0), samples s_base + s.
     // act == nullptr: slot a is pass tile tile0 + a / 64, lane a % 64, samples from 0.
@@ -2291,32 +2289,20 @@ __device__ __forceinline__ void first_pool(const SampleBuf& sb, int& pool_next, 
     pool_end = min(pool_next + sb.pool, sb.n_items);
     exhausted = pool_next >= sb.n_items;
 }
-// A wave's next item range [pool_next, pool_end) (wave-uniform; exhausted when none is
-// left). Items below sb.tail_from come from the first counter in takes of sb.pool items;
-// the launch's last items [tail_from, n_items) from a second counter in takes of
-// sb.tail_pool, so the waves that draw the last items hold less of them (the drain).
+// A wave's next item range [pool_next, pool_end) from the global counter (wave-uniform;
+// exhausted when none is left). (A second counter dealing the launch's last items in
+// smaller takes measured within noise of this, profiles/r03/tail/.)
 __device__ __forceinline__ void take_pool(const RenderOut& out, const SampleBuf& sb, int lane, int& pool_next,
                                           int& pool_end, bool& exhausted) {
-    if (pool_next < sb.tail_from) {
-        int base = 0;
-        if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64)) + (int)(gridDim.x * (blockDim.x / kWave)) * sb.pool;
-        if (base < sb.tail_from) {
-            pool_next = base;
-            pool_end = min(base + sb.pool, sb.tail_from);
-            return;
-        }
-    }
     int base = 0;
-    if (lane == 0) base = (int)atomicAdd(out.tile_counter + 1, (unsigned)sb.tail_pool);
-    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64)) + sb.tail_from;
+    if (lane == 0) base = (int)atomicAdd(out.tile_counter, (unsigned)sb.pool);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64)) + (int)(gridDim.x * (blockDim.x / kWave)) * sb.pool;
     if (base >= sb.n_items) {
         exhausted = true;
-        pool_next = pool_end = sb.n_items;
         return;
     }
     pool_next = base;
-    pool_end = min(base + sb.tail_pool, sb.n_items);
+    pool_end = min(base + sb.pool, sb.n_items);
 }
 
 template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
@@ -2947,13 +2933,7 @@ __global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRe
         if (t_cnt + h_cnt + n_cnt + nwalk == 0) break;
         // the stage of this trip (wave-uniform): full SHADE / START trips first, else walk
         // while there are rays, else whatever is left
-        // policy 1: when the idle walkers outnumber the rays to trace, shade / start what is
-        // there (a partial trip) rather than walk on with idle lanes
-        const bool starve = sb.wpolicy != 0 && t_cnt < kWave - nwalk && kWave - nwalk >= sb.min_ready &&
-                            (h_cnt > 0 || n_cnt > 0);
-        const int stage = h_cnt >= kWave ? 1 : n_cnt >= kWave ? 2
-                        : (!starve && (t_cnt > 0 || nwalk > 0)) ? 0
-                        : (h_cnt > 0 && h_cnt >= n_cnt) ? 1 : n_cnt > 0 ? 2 : h_cnt > 0 ? 1 : 0;
+        const int stage = h_cnt >= kWave ? 1 : n_cnt >= kWave ? 2 : (t_cnt > 0 || nwalk > 0) ? 0 : h_cnt > 0 ? 1 : 2;
         prof_trip<PP>(pf);
         psec<PP>(pf, PR_ACC);  // the previous trip's queue appends and stage choice
         if (stage == 0) {

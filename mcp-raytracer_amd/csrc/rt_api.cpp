@@ -495,7 +495,6 @@ struct rt_camera {
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
             sb.min_ready = std::min(env_int(v.wpool ? "RT_AMD_WREADY" : "RT_AMD_READY", v.wpool ? 16 : 48), kWave);
-            sb.wpolicy = env_int0("RT_AMD_WPOLICY", 0);  // policy 1 measured within noise (profiles/r03/wpool_hbm/)
         };
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
@@ -515,15 +514,6 @@ struct rt_camera {
             LaunchGeom gp = v.wpool ? gw : g;
             const int block = v.wpool ? kBlockWPool : v.pool ? kBlockPool : kBlockChunk;
             gp.grid = (int)std::max<long>(1, std::min<long>(items / block + 1, (long)cus));
-            // optional tail hand-out: the launch's last items - RT_AMD_TAIL quarter-rounds of takes,
-            // one round = every resident wave taking sb.pool items - in takes of RT_AMD_TAIL_POOL
-            // tile-chunks from a second counter. Off: against a true baseline every setting
-            // measured within noise (Cornell / spheres-500 rank shares, profiles/r03/tail/)
-            const long gwaves = (long)gp.grid * (block / kWave);
-            const long static_end = std::min<long>(gwaves * sb.pool, items);
-            const long tail_items = (long)std::max(env_int0("RT_AMD_TAIL", 0), 0) * gwaves * sb.pool / 4;
-            sb.tail_from = (int32_t)std::min<long>(items, std::max<long>(static_end, items - tail_items));
-            sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 2));
             DevScene Sp = S;
             if (v.pool) gp.lds_bytes = (size_t)S.lds_pool_off + pool_lds_bytes();
             if (v.wpool) {
@@ -581,11 +571,6 @@ struct rt_camera {
             }
             if (items >= (1l << 31) - (1l << 24)) throw std::runtime_error("wavefront pass too large");
             sb.n_items = (int32_t)items;
-            const long gwaves = P / kWave;
-            const long static_end = std::min<long>(gwaves * sb.pool, items);
-            const long tail_items = (long)std::max(env_int0("RT_AMD_TAIL", 0), 0) * gwaves * sb.pool / 4;
-            sb.tail_from = (int32_t)std::min<long>(items, std::max<long>(static_end, items - tail_items));
-            sb.tail_pool = kWave * std::max(1, env_int("RT_AMD_TAIL_POOL", 2));
             if (!first) hip_check(hipMemsetAsync(d_tile, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");
             ensure_wf((size_t)P);
             WfState W{};
