@@ -7,6 +7,9 @@
 #   wf_prof    rocprofv3 kernel stats: wavefront vs chunked, spheres-100k 2048² spp16
 #   wf_pmc     counter passes (VALU, lanes, waits, L2 hit): wavefront vs chunked
 #   tail_ab    rank-0 shares N = 1..8 (tools/rank_share.py) under $ARMS env settings -> profiles/r03/tail/
+#   adapt_jump adaptive bench lines (reference defaults) under RT_AMD_ADAPT_JUMP arms   -> profiles/r03/exp2/
+#              (the Cornell arms of exp2 ran a variant library, RT_AMD_VARIANT=<name>, built with
+#              _build.build_native(variant=..., defines=[...]))
 # $ARMS / $CFGS override the arms and configurations (lines "name ENV=V ..." / "name bench-args").
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 R=$(pwd)
@@ -62,5 +65,15 @@ PASSES
         env $envs timeout -k 10 200 python tools/rank_share.py $sc > $O/rs_${sc}_${arm}.log 2>&1 || exit $?
       done
     done ;;
+  adapt_jump)
+    export OUT=$O/ab
+    CFGS="${CFGS:-acornell --adaptive
+aspheres --scene spheres --spp 64 --depth 8 --adaptive
+arain --scene rain --width 1920 --spp 512 --depth 16 --adaptive}" ARMS="${ARMS:-j0 RT_AMD_ADAPT_JUMP=0
+j20 RT_AMD_ADAPT_JUMP=20
+j50 RT_AMD_ADAPT_JUMP=50
+j100 RT_AMD_ADAPT_JUMP=100
+j200 RT_AMD_ADAPT_JUMP=200}" STEPS=5 bash tools/ab_env.sh || exit $?
+    python tools/ab_table.py $OUT > $OUT/table.txt ;;
   *) echo "unknown experiment $1" >&2; exit 2 ;;
 esac
