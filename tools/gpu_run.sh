@@ -47,8 +47,8 @@ for step in "$@"; do
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
         --output-format csv -- python3 $R/bench.py --no-cpu > $R/$O/prof.log 2>&1) || exit $? ;;
-    valu) VALU_DIR=$O/valu bash tools/pmc_valu.sh "${CFGS4[@]:0:3}" "--precision fp32" || exit $? ;;
-    traffic) bash tools/pmc_traffic.sh "${CFGS4[@]:0:3}" || exit $? ;;
+    valu) VALU_DIR=$O/valu bash tools/pmc_valu.sh "${CFGS4[@]}" "--precision fp32" || exit $? ;;
+    traffic) bash tools/pmc_traffic.sh "${CFGS4[@]}" && cp -r gpurun_out/traffic $O/ || exit $? ;;
     rankshare)
       run 200 rank_share_cornell.log python tools/rank_share.py cornell || exit $?
       run 200 rank_share_spheres.log python tools/rank_share.py spheres || exit $? ;;
