@@ -7,6 +7,8 @@
 #   wf_prof    rocprofv3 kernel stats: wavefront vs chunked, spheres-100k 2048² spp16
 #   wf_pmc     counter passes (VALU, lanes, waits, L2 hit): wavefront vs chunked
 #   tail_ab    rank-0 shares N = 1..8 (tools/rank_share.py) under $ARMS env settings -> profiles/r03/tail/
+#   variant_ab parity tests (-k $KSEL) on the variant libraries in $VARIANTS, then bench arms
+#              (Cornell ref / fp32 unless $CFGS) for the product library and each variant
 #   adapt_jump adaptive bench lines (reference defaults) under RT_AMD_ADAPT_JUMP arms   -> profiles/r03/exp2/
 #              (the Cornell arms of exp2 ran a variant library, RT_AMD_VARIANT=<name>, built with
 #              _build.build_native(variant=..., defines=[...]))
@@ -65,6 +67,21 @@ PASSES
         env $envs timeout -k 10 200 python tools/rank_share.py $sc > $O/rs_${sc}_${arm}.log 2>&1 || exit $?
       done
     done ;;
+  variant_ab)
+    for v in $VARIANTS; do
+      RT_AMD_VARIANT=$v timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+        -p no:cacheprovider -k "${KSEL:-cornell or pool or brute or config1 or golden or random or full_size or fp32}" \
+        > $O/pytest_$v.log 2>&1 || exit $?
+    done
+    export OUT=$O/ab
+    A="base RT_AMD_VARIANT="
+    for v in $VARIANTS; do A="$A
+$v RT_AMD_VARIANT=$v"; done
+    CFGS="${CFGS:-cornell --steps 5
+cornellfp32 --precision fp32 --steps 5}" ARMS="$A" STEPS=5 bash tools/ab_env.sh || exit $?
+    CFGS="${CFGS:-cornell --steps 5
+cornellfp32 --precision fp32 --steps 5}" ARMS="$A" STEPS=5 OUT=$O/ab2 bash tools/ab_env.sh || exit $?
+    python tools/ab_table.py $OUT > $OUT/table.txt; python tools/ab_table.py $O/ab2 > $O/ab2/table.txt ;;
   adapt_jump)
     export OUT=$O/ab
     CFGS="${CFGS:-acornell --adaptive
