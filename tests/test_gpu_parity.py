@@ -428,6 +428,33 @@ def test_pool_host_gates_fall_back_bit_exact(rt, oracle, gpu, ro, kernel):
     assert_stats_identical(st, orc["stats"])
 
 
+def _cornell_plus_spheres(n_extra):
+    """Cornell with n_extra small Lambertian spheres on the floor (8 + n_extra primitives)."""
+    import copy
+    import raytracer_amd as rt
+    sd = copy.deepcopy(rt.generate_scene_data({"type": "cornell"}))
+    for k in range(n_extra):
+        sd["objects"].append({"type": "sphere", "pos": [-0.8 + 0.2 * k, -0.9, 0.3 - 0.1 * (k % 3)], "r": 0.08,
+                              "material": "sphere-white"})
+    return sd
+
+
+@pytest.mark.parametrize("n_extra,kernel", [(1, "pool"), (8, "chunked")])
+def test_pool_lds_budget_gate_falls_back_bit_exact(rt, oracle, gpu, n_extra, kernel):
+    """The pool kernel's LDS: fp16 candidate columns (primitives x 1024 x 2 B) + the level-2
+    scene + 16 waves x 152 path slots. Cornell + 1 sphere (9 primitives) still fits; Cornell +
+    8 (16 primitives: 32 KB of columns) does not, and rt_api.cpp's gate must hand the launch
+    to the chunked kernel - the same image either way."""
+    sd = _cornell_plus_spheres(n_extra)
+    ro = {"width": 48, "aspect": 1, "samples": 8, "depth": 10, **NOADAPT}
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    assert cam.info["traversal"] == 2  # AUTO -> brute force (<= 16 primitives)
+    assert cam.last_kernel() == kernel
+    orc = oracle.render(sd, ro)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"LDS gate +{n_extra} -> {kernel}")
+    assert_stats_identical(st, orc["stats"])
+
+
 def _tiny_scene(n):
     objs = [{"type": "sphere", "pos": [0.9 * k - 0.9, 0.3 * (k % 2), -0.2 * k], "r": 0.45, "material": "m"}
             for k in range(n)]
