@@ -196,12 +196,14 @@ static double js_random() {
 // ---------------------------------------------------------------------------
 template <class R> static inline R jmin(R a, R b) {
     if (a != a || b != b) return a + b;
-    if (a < b) return a; if (b < a) return b;
+    if (a < b) return a;
+    if (b < a) return b;
     return (a == 0 && b == 0) ? (std::signbit(a) ? a : b) : a;
 }
 template <class R> static inline R jmax(R a, R b) {
     if (a != a || b != b) return a + b;
-    if (a > b) return a; if (b > a) return b;
+    if (a > b) return a;
+    if (b > a) return b;
     return (a == 0 && b == 0) ? (std::signbit(a) ? b : a) : a;
 }
 template <class R> static inline R R_sqrt(R x) { return std::sqrt(x); }
@@ -1200,6 +1202,11 @@ void or_reflect(const double* v, const double* n, double* out) { put(out, V(v).r
 void or_refract(const double* v, const double* n, double eta, double* out) { put(out, V(v).refract(V(n), eta)); }
 void or_unit(const double* v, double* out) { put(out, V(v).unitVector()); }
 double or_length(const double* v) { return V(v).length(); }
+// ONBasis around n (src/geometry/onbasis.ts:18-51): out {u.xyz, v.xyz, w.xyz, local(a).xyz}
+void or_onb(const double* n, const double* a, double* out) {
+    ONB<double> b(V(n));
+    put(out, b.u); put(out + 3, b.v); put(out + 6, b.w); put(out + 9, b.local(V(a)));
+}
 // The oracle's Math.cos / Math.sin of the cosine-PDF angle phi = 2 * PI * xi,
 // xi = u / 2^32 (Vec3.randomCosineDirection, src/geometry/vec3.ts:325-337), and
 // Schlick's Math.pow(xi, 5) (src/materials/dielectric.ts:98): for the V8 fixture

@@ -66,6 +66,8 @@ def load():
         lib.or_unit.argtypes = [D, D]
         lib.or_length.argtypes = [D]
         lib.or_length.restype = C.c_double
+        lib.or_onb.argtypes = [D, D, D]
+        lib.or_onb.restype = None
         lib.or_mixture_value.argtypes = [C.c_int, D, D]
         lib.or_mixture_value.restype = C.c_double
         lib.or_rng_stream.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p]
@@ -202,6 +204,13 @@ def unit(v):
 
 def length(v):
     return load().or_length(_d(v))
+
+
+def onb(n, a=(0, 0, 0)):
+    """ONBasis(n): (u, v, w, local(a)) - src/geometry/onbasis.ts:18-51."""
+    out = (C.c_double * 12)()
+    load().or_onb(_d(n), _d(a), out)
+    return list(out[0:3]), list(out[3:6]), list(out[6:9]), list(out[9:12])
 
 
 def mixture_value(values, weights):

@@ -312,6 +312,27 @@ def _hit_equal(rt, oracle, sd, o, d, travs=("reference", "fast", "brute")):
     return c
 
 
+@pytest.mark.parametrize("spheres", [
+    [((0, 0, -1), 0.5), ((-1, 0, -1), 0.5), ((1, 0, -1), 0.5), ((0, -100.5, -1), 100)],  # bvh.test.ts:15-20
+    [((i - 5, 0, -5), 0.3) for i in range(10)],  # bvh.test.ts:23-28 (leaf)
+    [((0, 0, -3), 0.5), ((0, 0, -1), 0.5)],  # hittableList.test.ts:49-50, far sphere added first
+], ids=["bvh4", "bvh_leaf", "list2"])
+def test_reference_bvh_and_list_scenes(rt, oracle, gpu, spheres):
+    """The reference's BVH / HittableList test worlds through the product's
+    world_hit (every traversal) vs the oracle, on the tests' rays plus a fan."""
+    sd = {"camera": {"vfov": 90, "from": [0, 0, 0], "at": [0, 0, -1], "up": [0, 1, 0],
+                     "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [0.5, 0.7, 1]}},
+          "objects": [{"type": "sphere", "pos": list(c), "r": r,
+                       "material": {"type": "lambert", "color": [0.8, 0.8, 0.8]}} for c, r in spheres]}
+    rng = np.random.default_rng(3)
+    d = np.concatenate([np.float32([[0, 0, -1], [0, 1, 0], [0.408248, -0.408248, -0.816497]]),
+                        rng.normal(size=(509, 3)).astype(np.float32)])
+    o = np.zeros_like(d)
+    o[1] = (0, 5, 0)
+    c = _hit_equal(rt, oracle, sd, o, d)
+    assert c[0, 0] > 0 and c[1, 0] == 0
+
+
 def test_axis_quad_edges_and_corners(rt, oracle, gpu):
     """Cornell walls are axis-aligned quads (aquad_t): rays aimed exactly at
     edges, corners and just outside them must decide alpha/beta like the

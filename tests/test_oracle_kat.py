@@ -201,3 +201,129 @@ def test_rng_stream_product_matches_oracle(oracle, rt):
     """The seeded Math.random replacement: product (host) and oracle streams agree bit-for-bit."""
     for key in [(0x5EED, 0, 0), (1, 12345, 7), (0xFFFFFFFF, 4096 * 4096 - 1, 1023)]:
         assert rt.rng_stream(*key, 64) == oracle.rng_stream(*key, 64)
+
+
+# ---- tests/geometry/vec3.test.ts:81-110 ------------------------------------
+def test_vec3_length_and_unit_kats(oracle):
+    assert oracle.length((3, 4, 0)) == 5 and oracle.length((0, 0, 0)) == 0
+    assert close(oracle.length((1, 1, 1)), math.sqrt(3))
+    u = oracle.unit((3, 4, 0))
+    assert close(u[0], 3 / 5) and close(u[1], 4 / 5) and close(u[2], 0) and close(oracle.length(u), 1)
+
+
+# ---- tests/geometry/onbasis.test.ts:7-86 -----------------------------------
+def _dot(a, b):
+    return sum(x * y for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("n", [(0, 1, 0), (1, 0, 0), (0, 0, 1), (1, 1, 1), (-1, 2, 3)])
+def test_onbasis_kats(oracle, n):
+    n = oracle.unit(n)
+    u, v, w, _ = oracle.onb(n)
+    assert close(_dot(w, n), 1)
+    for a in (u, v, w):
+        assert close(oracle.length(a), 1)
+    assert close(_dot(u, v), 0) and close(_dot(u, w), 0) and close(_dot(v, w), 0)
+
+
+def test_onbasis_local_kats(oracle):
+    n = (0, 1, 0)
+    u, v, w, z = oracle.onb(n, (0, 0, 1))
+    assert close(_dot(z, n), 1)
+    x = oracle.onb(n, (1, 0, 0))[3]
+    y = oracle.onb(n, (0, 1, 0))[3]
+    assert close(_dot(x, n), 0) and close(_dot(y, n), 0) and close(_dot(y, x), 0)
+    c = oracle.onb(n, (1, 2, 3))[3]
+    want = [a + 2 * b + 3 * e for a, b, e in zip(u, v, w)]
+    assert all(close(a, b) for a, b in zip(c, want))
+
+
+# ---- tests/geometry/interval.test.ts:55-70 + src/entities/sphere.ts:60-62 --
+def test_hit_interval_is_open(oracle):
+    """Primitive hits use Interval.surrounds (strict): a root exactly at tmin
+    or tmax is rejected, so the far root is taken or the ray misses."""
+    c, r, o, d = (0, 0, -1), 0.5, (0, 0, 0), (0, 0, -1)
+    h = oracle.sphere_hit(c, r, o, d, 0.5, math.inf)
+    assert h["hit"] and h["t"] == 1.5
+    assert not oracle.sphere_hit(c, r, o, d, 0.001, 0.5)["hit"]
+    assert oracle.sphere_hit(c, r, o, d, 0.001, 0.5000001)["t"] == 0.5
+
+
+# ---- tests/geometry/hittableList.test.ts + tests/geometry/bvh.test.ts ------
+def _world(spheres):
+    return {"camera": {"vfov": 90, "from": [0, 0, 0], "at": [0, 0, -1], "up": [0, 1, 0],
+                       "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [0.5, 0.7, 1]}},
+            "objects": [{"type": "sphere", "pos": list(c), "r": r, "material": {"type": "lambert",
+                                                                                "color": [0.8, 0.8, 0.8]}}
+                        for c, r in spheres]}
+
+
+def _hit(oracle, spheres, o, d, tmin, tmax):
+    row = oracle.world_hit(_world(spheres), [o], [d], tmin, tmax)[0]
+    return {"hit": bool(row[0]), "t": row[1], "p": row[2:5], "obj": int(row[9])}
+
+
+def _brute(oracle, spheres, o, d, tmin, tmax):
+    """HittableList.hit (src/geometry/hittableList.ts:40-60): closest-so-far over the list."""
+    best = None
+    for i, (c, r) in enumerate(spheres):
+        h = oracle.sphere_hit(c, r, o, d, tmin, best["t"] if best else tmax)
+        if h["hit"]:
+            best = dict(h, obj=i)
+    return best
+
+
+S1, S2 = ((0, 0, -1), 0.5), ((0, 0, -3), 0.5)  # hittableList.test.ts:49-50
+
+
+def test_hittable_list_kats(oracle):
+    o, d = (0, 0, 0), (0, 0, -1)
+    far = ((0, 100, -5), 10)  # hittableList.test.ts:12-14
+    assert _hit(oracle, [S1], o, d, 0.001, math.inf)["hit"]
+    assert not _hit(oracle, [S1], (0, 100, 0), d, 0.001, math.inf)["hit"]
+    assert _hit(oracle, [S1, far], (0, 100, 0), d, 0.001, math.inf)["hit"]
+    assert not _hit(oracle, [S1], (5, 5, 0), d, 0.001, math.inf)["hit"]
+    h = _hit(oracle, [S1, S2], o, d, 0.001, math.inf)
+    assert close(h["t"], 0.5) and close(h["p"][2], -0.5) and h["obj"] == 0
+    h = _hit(oracle, [S2, S1], o, d, 0.001, math.inf)  # add order does not matter
+    assert close(h["t"], 0.5) and close(h["p"][2], -0.5) and h["obj"] == 1
+    assert close(_hit(oracle, [S1, S2], o, d, 0.001, 1.0)["t"], 0.5)
+    h = _hit(oracle, [S1, S2], o, d, 1.0, math.inf)  # sphere1's far root beats sphere2
+    assert close(h["t"], 1.5) and close(h["p"][2], -1.5)
+    assert not _hit(oracle, [S1, S2], o, d, 1.6, 2.4)["hit"]
+
+
+BVH_SPHERES = [((0, 0, -1), 0.5), ((-1, 0, -1), 0.5), ((1, 0, -1), 0.5), ((0, -100.5, -1), 100)]  # bvh.test.ts:15-20
+SMALL_SPHERES = [((i - 5, 0, -5), 0.3) for i in range(10)]  # bvh.test.ts:23-28
+
+
+def test_bvh_box_kat(oracle):
+    boxes = [oracle.prim_box("sphere", c, r=r) for c, r in BVH_SPHERES]
+    mn = [min(b[0][a] for b in boxes) for a in range(3)]
+    mx = [max(b[1][a] for b in boxes) for a in range(3)]
+    assert mn[0] <= -1.5 and mx[0] >= 1.5 and mn[1] <= -100.5 - 100
+
+
+def test_bvh_hit_kats(oracle):
+    h = _hit(oracle, BVH_SPHERES, (0, 0, 0), (0, 0, -1), 0.1, 100)
+    assert h["hit"] and close(h["t"], 0.5)
+    assert not _hit(oracle, BVH_SPHERES, (0, 5, 0), (0, 1, 0), 0.1, 100)["hit"]
+    assert _hit(oracle, SMALL_SPHERES, (0, 0, 0), (0, 0, -1), 0.1, 100)["hit"]
+
+
+@pytest.mark.parametrize("spheres", [BVH_SPHERES, SMALL_SPHERES], ids=["four", "leaf"])
+def test_bvh_matches_list(oracle, spheres):
+    """bvh.test.ts:89-158 - BVH and list agree (t bit-exact, same object), on the
+    test's rays plus a seeded fan of float32 rays."""
+    import numpy as np
+    rng = np.random.default_rng(11)
+    dirs = [oracle.unit((0.5, -0.5, -1)), (0, 0, -1)] + [list(v) for v in rng.normal(size=(200, 3))]
+    o = (0, 0, 0)
+    sd = _world(spheres)
+    D = np.asarray(dirs, dtype=np.float32)
+    rows = oracle.world_hit(sd, np.zeros_like(D), D, 0.1, 100)
+    for d, row in zip(D.astype(np.float64), rows):
+        b = _brute(oracle, spheres, o, d, 0.1, 100)
+        assert bool(row[0]) == (b is not None)
+        if b is not None:
+            assert row[1] == b["t"] and int(row[9]) == b["obj"]
