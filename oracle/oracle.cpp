@@ -1228,6 +1228,34 @@ double or_mixture_value(int n, const double* values, const double* weights) {
     MixturePDF<double> m(pp, ws);
     return m.value(Vec3<double>());
 }
+// One Material.scatter + emitted per trial (src/materials/*.ts), at a hit at the
+// origin with the given normal / front flag, incoming direction `din`. Trial k
+// draws from Rng::for_path(seed, k, 0). out[k*12..]: {valid, hasScattered,
+// reflected, attenuation.xyz, dir.xyz, emitted.xyz}; dir is the scattered ray's
+// direction, or pdf.generate() for a PDF result (tests/materials/*.test.ts).
+int or_material_probe(const char* material_json, const double* din, const double* normal, int front, uint32_t seed,
+                      int n, double* out) {
+    try {
+        J md = parse_json(material_json);
+        Scene<double> scene;
+        const Material<double>* m = scene.create_material(&md);
+        HitRecord<double> rec; rec.p = Vec3<double>::create(0, 0, 0); rec.normal = V(normal); rec.t = 1;
+        rec.frontFace = front != 0; rec.material = m;
+        Ray<double> rin{Vec3<double>::create(0, 0, 0).subtract(V(din)), V(din)};
+        for (int k = 0; k < n; k++) {
+            Rng rng = Rng::for_path(seed, (uint32_t)k, 0);
+            g_rng = &rng;
+            double* o = out + k * 12;
+            ScatterResult<double> s = m->scatter(rin, rec);
+            o[0] = s.valid; o[1] = s.hasScattered; o[2] = s.reflected;
+            put(o + 3, s.valid ? s.attenuation : Vec3<double>());
+            put(o + 6, !s.valid ? Vec3<double>() : s.hasScattered ? s.scattered.direction : s.pdf->generate());
+            put(o + 9, m->emitted(rec));
+            g_rng = nullptr;
+        }
+        return 0;
+    } catch (const std::exception& e) { g_rng = nullptr; g_err = e.what(); return 1; }
+}
 // RNG stream (for cross-checking the device RNG bit-for-bit)
 void or_rng_stream(uint32_t seed, uint32_t pixel, uint32_t sample, int n, uint32_t* out) {
     Rng r = Rng::for_path(seed, pixel, sample);

@@ -67,6 +67,7 @@ def load():
         lib.or_length.argtypes = [D]
         lib.or_length.restype = C.c_double
         lib.or_onb.argtypes = [D, D, D]
+        lib.or_material_probe.argtypes = [C.c_char_p, D, D, C.c_int, C.c_uint32, C.c_int, C.c_void_p]
         lib.or_onb.restype = None
         lib.or_mixture_value.argtypes = [C.c_int, D, D]
         lib.or_mixture_value.restype = C.c_double
@@ -211,6 +212,17 @@ def onb(n, a=(0, 0, 0)):
     out = (C.c_double * 12)()
     load().or_onb(_d(n), _d(a), out)
     return list(out[0:3]), list(out[3:6]), list(out[6:9]), list(out[9:12])
+
+
+def material_probe(material: dict, din, normal, front=True, seed=1, n=1):
+    """n trials of Material.scatter + emitted (src/materials/*.ts) at a hit at the
+    origin: array (n, 12) = valid, hasScattered, reflected, attenuation.xyz,
+    direction.xyz (scattered ray or pdf.generate()), emitted.xyz."""
+    out = np.zeros((n, 12), dtype=np.float64)
+    if load().or_material_probe(json.dumps(material).encode(), _d(din), _d(normal), int(bool(front)), seed, n,
+                                out.ctypes.data):
+        raise _err()
+    return out
 
 
 def mixture_value(values, weights):

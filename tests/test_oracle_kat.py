@@ -6,6 +6,8 @@ toBeCloseTo(x, p) means |d| < 10**-p / 2.
 """
 import math
 
+import numpy as np
+
 import pytest
 
 
@@ -150,7 +152,6 @@ def test_vec3_boundary(oracle):
     u = oracle.unit((1, 2, 2))
     assert all(close(a, b, 6) for a, b in zip(u, (1 / 3, 2 / 3, 2 / 3)))
     # fp32 storage: components are exactly representable floats
-    import numpy as np
     assert all(np.float32(a) == a for a in u)
     r = oracle.refract((0, -1, 0), (0, 1, 0), 1 / 1.5)  # normal incidence passes straight through
     assert all(close(a, b, 6) for a, b in zip(r, (0, -1, 0)))
@@ -315,7 +316,6 @@ def test_bvh_hit_kats(oracle):
 def test_bvh_matches_list(oracle, spheres):
     """bvh.test.ts:89-158 - BVH and list agree (t bit-exact, same object), on the
     test's rays plus a seeded fan of float32 rays."""
-    import numpy as np
     rng = np.random.default_rng(11)
     dirs = [oracle.unit((0.5, -0.5, -1)), (0, 0, -1)] + [list(v) for v in rng.normal(size=(200, 3))]
     o = (0, 0, 0)
@@ -327,3 +327,97 @@ def test_bvh_matches_list(oracle, spheres):
         assert bool(row[0]) == (b is not None)
         if b is not None:
             assert row[1] == b["t"] and int(row[9]) == b["obj"]
+
+
+# ---- tests/materials/*.test.ts: Material.scatter / emitted ------------------
+# material_probe rows: valid, hasScattered, reflected, attenuation.xyz, dir.xyz, emitted.xyz
+RED = {"type": "lambert", "color": [0.8, 0.2, 0.2]}
+SILVER = {"type": "metal", "color": [0.9, 0.9, 0.9], "fuzz": 0.1}
+GLASS = {"type": "glass", "ior": 1.5}
+
+
+def test_diffuse_light_kats(oracle):
+    """diffuseLight.test.ts:7-59 - emits its colour, never scatters."""
+    r = oracle.material_probe({"type": "light", "emit": [3, 2, 1]}, (0, 1, 0), (0, 1, 0), n=4)
+    assert (r[:, 0] == 0).all() and (r[:, 9:12] == [3, 2, 1]).all()
+
+
+def test_non_emitting_materials_emit_black(oracle):
+    """defaultMaterial.test.ts:26-40 / layeredMaterial.test.ts:188-201 /
+    mixedMaterial.test.ts:242-253: only lights emit."""
+    for m in [RED, SILVER, GLASS, {"type": "mixed", "diff": RED, "spec": SILVER, "weight": 0.5},
+              {"type": "layered", "outer": GLASS, "inner": RED}]:
+        assert (oracle.material_probe(m, (0, -1, 0), (0, 1, 0))[:, 9:12] == 0).all(), m["type"]
+
+
+def test_lambertian_kats(oracle):
+    """lambertian.test.ts:9-125 - albedo attenuation, cosine-PDF directions in the normal's hemisphere."""
+    r = oracle.material_probe({"type": "lambert", "color": [0.5, 0.7, 0.3]}, (0, 1, 0), (0, 1, 0), n=200)
+    assert (r[:, 0] == 1).all() and (r[:, 1] == 0).all()
+    assert np.allclose(r[:, 3:6], np.float32([0.5, 0.7, 0.3]))
+    assert (r[:, 7] > 0).all() and np.allclose(np.linalg.norm(r[:, 6:9], axis=1), 1, atol=0.05)
+
+
+def test_metal_fuzz_kats(oracle):
+    """metal.test.ts:77-125 - fuzz perturbs the mirror direction, which stays outward."""
+    r = oracle.material_probe({"type": "metal", "color": [0.8, 0.6, 0.2], "fuzz": 0.5}, (0, -1, 0), (0, 1, 0), n=100)
+    ok = r[:, 0] == 1
+    assert ok.all() and (r[:, 7] > 0).all()
+    perfect = (np.abs(r[:, 6]) < 1e-3) & (np.abs(r[:, 7] - 1) < 1e-3) & (np.abs(r[:, 8]) < 1e-3)
+    assert perfect.sum() < 10
+
+
+def test_metal_absorbs_below_surface(oracle):
+    """metal.test.ts:127-160 - a grazing ray with heavy fuzz is absorbed
+    (null) whenever the fuzzed reflection points below the surface."""
+    d = oracle.unit((1, -0.01, 0))
+    r = oracle.material_probe({"type": "metal", "color": [0.8, 0.6, 0.2], "fuzz": 0.8}, d, (0, 1, 0), n=400)
+    assert 0 < (r[:, 0] == 0).sum() < 400  # some absorbed, some not
+    assert (r[r[:, 0] == 1, 7] > 0).all()
+
+
+def test_dielectric_scatter_kats(oracle):
+    """dielectric.test.ts:16-107 - always a scattered ray, entering and exiting; white attenuation."""
+    g = {"type": "glass", "ior": 1.5}
+    for din, front in [((0, 0, -1), True), ((0, 0, 1), False)]:
+        r = oracle.material_probe(g, din, (0, 0, 1), front, n=50)
+        assert (r[:, 0] == 1).all() and (r[:, 1] == 1).all() and (r[:, 3:6] == 1).all()
+        assert (np.linalg.norm(r[:, 6:9], axis=1) > 0).all()
+    r = oracle.material_probe({"type": "glass", "ior": 2.4}, oracle.unit((0.9, 0.1, 0)), (-1, 0, 0), False, n=50)
+    assert (r[:, 0] == 1).all() and (np.linalg.norm(r[:, 6:9], axis=1) > 0).all()
+    # ratio * sin(theta) > 1: total internal reflection on every trial
+    r = oracle.material_probe({"type": "glass", "ior": 2.4}, oracle.unit((1, -0.3, 0)), (0, 1, 0), False, n=50)
+    assert (r[:, 2] == 1).all()
+
+
+def test_mixed_material_kats(oracle):
+    """mixedMaterial.test.ts:49-130,214-240 - weight clamps to [0,1]; weight 1 is
+    always material1 (PDF), 0 always material2 (scattered ray); 0.3 splits ~30/70;
+    emission is the weighted sum."""
+    mix = lambda w: {"type": "mixed", "diff": RED, "spec": SILVER, "weight": w}
+    for w, want_pdf in [(1.0, True), (1.5, True), (0.0, False), (-0.5, False)]:
+        r = oracle.material_probe(mix(w), (1, -1, 0), (0, 1, 0), n=20)
+        valid = r[:, 0] == 1
+        assert valid.all()
+        assert ((r[:, 1] == 0) == want_pdf).all(), w
+    r = oracle.material_probe(mix(0.3), (1, -1, 0), (0, 1, 0), n=2000)
+    assert abs((r[:, 1] == 0).mean() - 0.3) < 0.05
+    e = oracle.material_probe({"type": "mixed", "weight": 0.3, "diff": {"type": "light", "emit": [1, 1, 0]},
+                               "spec": {"type": "light", "emit": [0, 1, 1]}}, (0, -1, 0), (0, 1, 0))[0, 9:12]
+    assert all(close(a, b, 5) for a, b in zip(e, (0.3, 1.0, 0.7)))
+
+
+def test_layered_material_kats(oracle):
+    """layeredMaterial.test.ts:57-260 - a dielectric reflection returns white
+    attenuation and a ray; a transmission hands the refracted ray to the
+    inner material (Lambertian: its albedo + PDF; Metal: its albedo + ray)."""
+    lay = {"type": "layered", "outer": GLASS, "inner": RED}
+    r = oracle.material_probe(lay, (1, 0, 0), (-1, 0, 0), n=1000)
+    refl = (r[:, 1] == 1) & (r[:, 3:6] == 1).all(axis=1)
+    paint = (r[:, 1] == 0) & np.isclose(r[:, 3:6], np.float32([0.8, 0.2, 0.2])).all(axis=1)
+    assert refl.sum() > 0 and paint.sum() > 0 and refl.sum() + paint.sum() == 1000
+    metal = {"type": "metal", "color": [0.8, 0.8, 0.9], "fuzz": 0.1}
+    r = oracle.material_probe({"type": "layered", "outer": GLASS, "inner": metal}, (1, -1, 0), (0, 1, 0), n=1000)
+    glass = (r[:, 1] == 1) & (r[:, 3:6] == 1).all(axis=1)
+    through = (r[:, 1] == 1) & np.isclose(r[:, 3:6], np.float32([0.8, 0.8, 0.9])).all(axis=1)
+    assert glass.sum() > 0 and through.sum() > 0
