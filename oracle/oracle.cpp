@@ -1256,6 +1256,22 @@ int or_material_probe(const char* material_json, const double* din, const double
         return 0;
     } catch (const std::exception& e) { g_rng = nullptr; g_err = e.what(); return 1; }
 }
+// Camera.getRay(i, j) of sample n (src/camera.ts getRay), the RNG keyed as in a
+// render (Rng::for_path(seed, j * W + i, n)): out[6] = {origin.xyz, direction.xyz}.
+int or_get_ray(const char* scene_json, const char* render_json, int i, int j, int n, double* out) {
+    try {
+        J sd = parse_json(scene_json);
+        J ro; bool has = render_json && render_json[0]; if (has) ro = parse_json(render_json);
+        auto cam = std::make_unique<Camera<double>>();
+        cam->load(sd, has ? &ro : nullptr);
+        Rng rng = Rng::for_path(cam->seed, (uint32_t)j * (uint32_t)cam->W + (uint32_t)i, (uint32_t)n);
+        g_rng = &rng;
+        Ray<double> r = cam->getRay(i, j);
+        g_rng = nullptr;
+        put(out, r.origin); put(out + 3, r.direction);
+        return 0;
+    } catch (const std::exception& e) { g_rng = nullptr; g_err = e.what(); return 1; }
+}
 // RNG stream (for cross-checking the device RNG bit-for-bit)
 void or_rng_stream(uint32_t seed, uint32_t pixel, uint32_t sample, int n, uint32_t* out) {
     Rng r = Rng::for_path(seed, pixel, sample);

@@ -67,6 +67,7 @@ def load():
         lib.or_length.argtypes = [D]
         lib.or_length.restype = C.c_double
         lib.or_onb.argtypes = [D, D, D]
+        lib.or_get_ray.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, D]
         lib.or_material_probe.argtypes = [C.c_char_p, D, D, C.c_int, C.c_uint32, C.c_int, C.c_void_p]
         lib.or_onb.restype = None
         lib.or_mixture_value.argtypes = [C.c_int, D, D]
@@ -233,6 +234,15 @@ def rng_stream(seed, pixel, sample, n):
     out = (C.c_uint32 * n)()
     load().or_rng_stream(seed, pixel, sample, n, out)
     return list(out)
+
+
+def get_ray(scene: dict, render_opts: dict | None, i: int, j: int, n: int = 0):
+    """Camera.getRay(i, j) of sample n (src/camera.ts), RNG keyed as in a render: (origin, direction)."""
+    out = (C.c_double * 6)()
+    if load().or_get_ray(json.dumps(scene).encode(), json.dumps(render_opts).encode() if render_opts else b"", i, j, n,
+                         out):
+        raise _err()
+    return list(out[0:3]), list(out[3:6])
 
 
 def camera_info(scene: dict, render_opts: dict | None = None):

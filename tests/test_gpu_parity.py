@@ -1131,3 +1131,42 @@ def test_wavefront_spheres100k_2048_rows_match_oracle(rt, oracle, gpu, monkeypat
         orc = oracle.render(sd, ro, region=(x, y, 16, 1), threads=16)
         assert_identical(rad[y:y + 1, x:x + 16], rgb[y:y + 1, x:x + 16], orc["radiance"][y:y + 1, x:x + 16],
                          orc["rgb"][y:y + 1, x:x + 16], f"spheres-100k 2048^2 row {y} x {x}")
+
+
+# ---------------------------------------------------------------------------
+# The camera configurations of the reference's camera.test.ts (defocus, focus
+# distance, orientations incl. a view direction parallel to `up`, roulette off /
+# early, zero and >1 albedo) through the product path, bit-exact vs the oracle.
+# ---------------------------------------------------------------------------
+def _cam_scene(albedo=0.5, **cam):
+    c = {"vfov": 90, "from": [0, 0, 0], "at": [0, 0, -1], "up": [0, 1, 0],
+         "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [0.5, 0.7, 1.0]}}
+    c.update(cam)
+    return {"camera": c, "materials": [{"id": "m", "material": {"type": "lambert", "color": [albedo] * 3}}],
+            "objects": [{"type": "sphere", "pos": [0, 0, -1], "r": 0.5, "material": "m"}]}
+
+
+CAMERA_CASES = {  # name: (scene kwargs, render options) - camera.test.ts line ranges
+    "aperture0": ({"aperture": 0}, {}),                                        # 202-222
+    "aperture2_focus1": ({"aperture": 2.0, "focus": 1.0}, {"samples": 10}),    # 224-248
+    "auto_focus": ({"from": [0, 0, 3], "at": [0, 0, 0], "aperture": 1.0}, {}),  # 176-187
+    "aperture_tiny": ({"aperture": 0.001, "focus": 1.0}, {}),                  # 278-289
+    "aperture_large": ({"aperture": 10.0, "focus": 1.0}, {}),                  # 290-300
+    "orient_diag": ({"from": [1, 1, 1], "at": [0, 0, 0], "aperture": 1.0}, {}),  # 417-439
+    "orient_up_parallel": ({"from": [0, 5, 0], "at": [0, 0, 0], "aperture": 1.0}, {}),
+    "roulette_off": ({}, {"roulette": False, "samples": 16}),                  # 592-624
+    "roulette_depth2": ({}, {"roulette": True, "rouletteDepth": 2, "samples": 16}),  # 628-654
+    "zero_albedo": ({"albedo": 0.0}, {"rouletteDepth": 1}),                    # 658-677
+    "high_albedo": ({"albedo": 2.0}, {"rouletteDepth": 1}),                    # 679-698
+}
+
+
+@pytest.mark.parametrize("case", sorted(CAMERA_CASES))
+def test_reference_camera_configurations_match_oracle(rt, oracle, gpu, case):
+    kw, extra = CAMERA_CASES[case]
+    sd = _cam_scene(**kw)
+    ro = {"width": 24, "aspect": 1.0, "samples": 4, "depth": 10, **NOADAPT, **extra}
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
+    orc = oracle.render(sd, ro)
+    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"camera {case} ({cam.last_kernel()})")
+    assert_stats_identical(st, orc["stats"])

@@ -421,3 +421,89 @@ def test_layered_material_kats(oracle):
     glass = (r[:, 1] == 1) & (r[:, 3:6] == 1).all(axis=1)
     through = (r[:, 1] == 1) & np.isclose(r[:, 3:6], np.float32([0.8, 0.8, 0.9])).all(axis=1)
     assert glass.sum() > 0 and through.sum() > 0
+
+
+# ---- tests/camera.test.ts: getRay, defocus, orientations, roulette ---------
+def _cam_scene(**cam):
+    """createTestSceneData (camera.test.ts:99-131): one grey Lambertian sphere at (0, 0, -1)."""
+    c = {"vfov": 90, "from": [0, 0, 0], "at": [0, 0, -1], "up": [0, 1, 0],
+         "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [0.5, 0.7, 1.0]}}
+    c.update(cam)
+    return {"camera": c, "materials": [{"id": "test-material", "material": {"type": "lambert", "color": [0.5] * 3}}],
+            "objects": [{"type": "sphere", "pos": [0, 0, -1], "r": 0.5, "material": "test-material"}]}
+
+
+RD = {"width": 100, "aspect": 1.0, "samples": 1}  # camera.test.ts:153-157
+
+
+def _add(a, b):
+    return [x + y for x, y in zip(a, b)]
+
+
+def test_get_ray_aperture_zero_is_deterministic(oracle):
+    """camera.test.ts:202-222 - aperture 0, samples 1: every sample's ray is the same."""
+    sd = _cam_scene(aperture=0)
+    r0 = oracle.get_ray(sd, RD, 50, 50, 0)
+    assert all(oracle.get_ray(sd, RD, 50, 50, n) == r0 for n in range(1, 8))
+
+
+def test_get_ray_defocus_varies_origins_and_keeps_focus(oracle):
+    """camera.test.ts:176-276 - aperture > 0 moves ray origins over the lens; every ray
+    of a pixel still passes through the same point of the focus plane (samples 1: no
+    jitter), which sits |from - at| away unless `focus` is given."""
+    sd = _cam_scene(aperture=2.0, focus=1.0)
+    rays = [oracle.get_ray(sd, {**RD, "samples": 10}, 50, 50, n) for n in range(10)]
+    assert len({tuple(o) for o, _ in rays}) > 1
+    for from_, at, focus, plane_z in [([0, 0, 3], [0, 0, 0], None, 0.0), ([0, 0, 3], [0, 0, 0], 5.0, -2.0)]:
+        sd = _cam_scene(**{"from": from_, "at": at, "aperture": 1.0, **({"focus": focus} if focus else {})})
+        pts = [_add(*oracle.get_ray(sd, RD, 50, 50, n)) for n in range(6)]
+        assert len({tuple(o) for o, _ in (oracle.get_ray(sd, RD, 50, 50, n) for n in range(6))}) > 1
+        for p in pts:
+            assert all(close(a, b, 6) for a, b in zip(p, pts[0]))
+            assert close(p[2], plane_z, 6)
+
+
+@pytest.mark.parametrize("aperture", [0.001, 10.0])
+def test_get_ray_aperture_edge_cases(oracle, aperture):
+    """camera.test.ts:278-300."""
+    o, d = oracle.get_ray(_cam_scene(aperture=aperture, focus=1.0), RD, 50, 50, 3)
+    assert all(math.isfinite(x) for x in o + d) and oracle.length(d) > 0
+
+
+def test_get_ray_image_bounds_and_distinct_pixels(oracle):
+    """camera.test.ts:304-330 - corner pixels give finite non-zero directions; pixels differ."""
+    sd = _cam_scene()
+    ds = [tuple(oracle.get_ray(sd, RD, i, j)[1]) for i, j in [(0, 0), (99, 0), (0, 99), (99, 99), (50, 50)]]
+    assert all(oracle.length(d) > 0 for d in ds) and len(set(ds)) == 5
+    assert ds[0][0] < 0 < ds[1][0] and ds[0][1] > 0 > ds[2][1]  # row 0 is the top of the image
+
+
+@pytest.mark.parametrize("from_,at", [([0, 0, 1], [0, 0, 0]), ([1, 1, 1], [0, 0, 0]), ([-1, 0, 0], [1, 0, 0]),
+                                      ([0, 5, 0], [0, 0, 0])])
+def test_get_ray_orientations(oracle, from_, at):
+    """camera.test.ts:417-439 - the centre pixel looks along at - from."""
+    o, d = oracle.get_ray(_cam_scene(**{"from": from_, "at": at}), {**RD, "width": 101}, 50, 50)
+    look = oracle.unit([b - a for a, b in zip(from_, at)])
+    assert all(close(a, b, 6) for a, b in zip(oracle.unit(d), look)) and o == [float(x) for x in from_]
+
+
+def test_roulette_reduces_bounces(oracle):
+    """camera.test.ts:592-654 - Russian roulette keeps every pixel and does not add bounces."""
+    sd = _cam_scene()
+    for spp, rdepth, tol in [(100, 3, 1.2), (50, 2, 1.1)]:
+        off = oracle.render(sd, {"width": 10, "aspect": 1.0, "samples": spp, "roulette": False, "aTolerance": 0})
+        on = oracle.render(sd, {"width": 10, "aspect": 1.0, "samples": spp, "roulette": True, "rouletteDepth": rdepth,
+                                "aTolerance": 0})
+        assert off["stats"]["pixels"] == on["stats"]["pixels"] == 100
+        assert on["stats"]["bounces"]["total"] <= off["stats"]["bounces"]["total"] * tol
+
+
+@pytest.mark.parametrize("albedo", [0.0, 2.0])
+def test_roulette_zero_and_high_attenuation(oracle, albedo):
+    """camera.test.ts:658-698 - zero and >1 attenuation render finite radiance (continuation
+    probability capped at 0.95)."""
+    sd = _cam_scene()
+    sd["materials"][0]["material"]["color"] = [albedo] * 3
+    out = oracle.render(sd, {"width": 10, "aspect": 1.0, "samples": 8, "roulette": True, "rouletteDepth": 1,
+                             "aTolerance": 0})
+    assert np.isfinite(out["radiance"]).all() and (out["radiance"] >= 0).all()
