@@ -1170,3 +1170,47 @@ def test_reference_camera_configurations_match_oracle(rt, oracle, gpu, case):
     orc = oracle.render(sd, ro)
     assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"camera {case} ({cam.last_kernel()})")
     assert_stats_identical(st, orc["stats"])
+
+
+def _raytracer_test_scene():
+    """createTestSceneData of the reference's raytracer.test.ts:7-37."""
+    return {"camera": {"vfov": 40, "from": [0, 0, 2], "at": [0, 0, -1], "up": [0, 1, 0],
+                       "background": {"type": "gradient", "top": [1, 1, 1], "bottom": [0.5, 0.7, 1.0]}},
+            "materials": [{"id": "test-material", "material": {"type": "lambert", "color": [0.7, 0.3, 0.3]}}],
+            "objects": [{"type": "sphere", "pos": [0, 0, -1], "r": 0.5, "material": "test-material"}]}
+
+
+RAYTRACER_CASES = [  # (scene config, generateImageBuffer options, expected size) - raytracer.test.ts
+    ({"type": "custom", "render": {"width": 10, "aspect": 1.0, "samples": 1}}, {}, (10, 10)),        # 38-58
+    ({"type": "spheres", "render": {"width": 8, "aspect": 2.0, "samples": 1},
+      "options": {"count": 5, "seed": 12345}}, {}, (8, 4)),                                          # 60-82
+    ({"type": "custom", "render": {"width": 16, "aspect": 1.0, "samples": 1}}, {}, (16, 16)),        # 84-108
+    ({"type": "custom", "render": {"width": 20, "aspect": 2.0, "samples": 1}}, {}, (20, 10)),
+    ({"type": "custom", "render": {"width": 30, "aspect": 1.5, "samples": 1}}, {}, (30, 20)),
+    ({"type": "spheres", "render": {"width": 6, "aspect": 1.0, "samples": 1},
+      "options": {"count": 3, "seed": 42}}, {}, (6, 6)),                                             # 110-145
+    ({"type": "spheres", "render": {"width": 12, "aspect": 1.0, "samples": 2},
+      "options": {"count": 3, "seed": 54321}}, {"parallel": True, "threads": 2}, (12, 12)),          # 147-173
+    ({"type": "spheres", "render": {"width": 12, "aspect": 1.0, "samples": 20, "aTolerance": 0.1},
+      "options": {"count": 3, "seed": 54321}}, {}, (12, 12)),                                        # 175-
+]
+
+
+@pytest.mark.parametrize("k", range(len(RAYTRACER_CASES)))
+def test_reference_raytracer_cases_png_matches_oracle(rt, oracle, gpu, k):
+    """generateImageBuffer on the reference's raytracer.test.ts configurations: a PNG of
+    the stated size whose pixels are the oracle's render of the same scene, bit for bit."""
+    from raytracer_amd.png import decode_png_rgb
+    cfg, opts, (W, H) = RAYTRACER_CASES[k]
+    cfg = dict(cfg)
+    if cfg["type"] == "custom":
+        cfg["data"] = _raytracer_test_scene()
+        sd = cfg["data"]
+    else:
+        sd = rt.generate_scene_data({"type": cfg["type"], "options": cfg["options"]})
+    png = rt.generate_image_buffer(cfg, opts)
+    assert png[:8] == b"\x89PNG\r\n\x1a\n"
+    w, h, px = decode_png_rgb(png)
+    assert (w, h) == (W, H)
+    orc = oracle.render(sd, cfg["render"])
+    assert px == np.ascontiguousarray(orc["rgb"]).tobytes()
