@@ -2023,21 +2023,13 @@ __device__ __forceinline__ void publish_counters(const RenderOut& out, const uin
     }
 }
 
-// Workgroup prologue shared by the render kernels: LDS-resident scene data
-// (one cooperative copy per workgroup) and this thread's stack columns.
-// LDSS 0: all scene reads from global memory; 1: the traversal data and the
-// primitive records in LDS; 2: also the material and light tables; 3 (walker-pool
-// kernel): the traversal data only ([tnodes][tprims][tsph]), primitive records global. (Wave-
-// uniform reads - the brute-force primitive loop, the light list - stay on
-// scalar loads from the global copy.)
+// The scene as the kernel sees it after scene_prologue: LDS-resident arrays at their
+// LDS addresses (the prologue's copy of the blob prefix), the rest global.
 template <int LDSS>
-__device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
+__device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stack) {
     DevScene S = S0;
     if (LDSS > 0) {
-        uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
-        for (int w = threadIdx.x; w < S0.lds_words; w += blockDim.x) dst[w] = S0.blob[w];
-        __syncthreads();
-        const char* b = reinterpret_cast<const char*>(dst);
+        const char* b = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
         S.tsph = reinterpret_cast<const float4*>(b + S0.off_tsph);
@@ -2049,6 +2041,23 @@ __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_
         }
     }
     return S;
+}
+
+// Workgroup prologue shared by the render kernels: LDS-resident scene data
+// (one cooperative copy per workgroup) and this thread's stack columns.
+// LDSS 0: all scene reads from global memory; 1: the traversal data and the
+// primitive records in LDS; 2: also the material and light tables; 3 (walker-pool
+// kernel): the traversal data only ([tnodes][tprims][tsph]), primitive records global. (Wave-
+// uniform reads - the brute-force primitive loop, the light list - stay on
+// scalar loads from the global copy.)
+template <int LDSS>
+__device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
+    if (LDSS > 0) {
+        uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
+        for (int w = threadIdx.x; w < S0.lds_words; w += blockDim.x) dst[w] = S0.blob[w];
+        __syncthreads();
+    }
+    return scene_view<LDSS>(S0, lds_stack);
 }
 
 // ---------------------------------------------------------------------------
@@ -2307,6 +2316,31 @@ __device__ __forceinline__ void take_pool(const RenderOut& out, const SampleBuf&
     pool_end = min(base + sb.pool, sb.n_items);
 }
 
+#ifndef RT_CHUNK_KOPQ
+#define RT_CHUNK_KOPQ 1  // 0: the A/B arm that keeps the launch parameters in SGPRs (profiles/r03/exp5_ckopq/)
+#endif
+// The chunked kernel's parameters as one block (the kernarg segment has this struct's layout).
+// With RT_CHUNK_KOPQ its trip loop reads them through an opaque kernarg pointer at each use
+// (scalar loads from the constant cache) instead of keeping them live across the loop, where
+// the compiler ran out of SGPRs (106), spilled ~75 of them to VGPR lanes (v_writelane /
+// v_readlane, VALU issue) and spilled VGPRs to scratch: SGPR spills 72-75 -> 34-40 in the
+// fast-traversal builds; spheres-100k 2048^2 spp16 39.97 -> 38.55 ms, rain 11.65 -> 11.56 ms,
+// spheres-500 unchanged (profiles/r03/exp5_ckopq/). The same change in the pool kernel (SGPR
+// spills 97 -> 48) was within noise on Cornell ref and 1 % slower in fp32
+// (profiles/r03/exp4_kopq/), so the pool kernel keeps its parameters in registers.
+struct KernArgs {
+    DevScene S0;
+    RtRegion reg;
+    RenderOut out;
+    int tiles_x;
+    SampleBuf sb;
+};
+__device__ __forceinline__ const KernArgs& kern_args() {
+    KArgPtr p = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const KernArgs*)p;
+}
+
 template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
 __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRegion reg, RenderOut out,
                                                                         int tiles_x, SampleBuf sb) {
@@ -2349,21 +2383,32 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     FastWalk<Real> W;
     bool walking = false;
 
+#if RT_CHUNK_KOPQ
+#define PK_SB (kern_args().sb)
+#define PK_REG (kern_args().reg)
+#define PK_OUT (kern_args().out)
+#define PK_S (scene_view<LDSS>(kern_args().S0, lds_stack))
+#else
+#define PK_SB sb
+#define PK_REG reg
+#define PK_OUT out
+#define PK_S S
+#endif
     while (true) {
         // hand out items to idle lanes (wave-uniform control flow); waits until
         // refill_min lanes are idle so the hand-out cost is shared
         const unsigned long long need = __ballot(slot < 0);
         const int n_need = __popcll(need);
-        if (n_need != 0 && !exhausted && (n_need >= sb.refill_min || __ballot(slot >= 0) == 0ull)) {
-            if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
+        if (n_need != 0 && !exhausted && (n_need >= PK_SB.refill_min || __ballot(slot >= 0) == 0ull)) {
+            if (pool_next >= pool_end) take_pool(PK_OUT, PK_SB, lane, pool_next, pool_end, exhausted);
             if (!exhausted) {
                 const int take = min(n_need, pool_end - pool_next);
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 if (slot < 0 && rank < take) {
                     int tl, l, s1, e1;
-                    item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
-                    if (slot_pixel(sb, reg, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
+                    item_decode(PK_SB, ptab, pool_next + rank, tl, l, s1, e1);
+                    if (slot_pixel(PK_SB, PK_REG, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
                         slot = tl * 64 + l;
                         s = s1;
                         s_end = e1;
@@ -2388,7 +2433,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 r.y = c.y;
                 r.z = c.z;
                 r.w = __int_as_float(P.bounces);
-                rec_store<false>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
+                rec_store<false>(PK_SB.rec + ((size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot), r);
                 ++s;
                 if (s < s_end) new_path = true;
                 else slot = -1;
@@ -2399,7 +2444,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             // cut-off / roulette, and the walk of its ray
             if (slot >= 0 && !walking) {
                 if (new_path) {
-                    path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(sb.s_base + s));
+                    path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(PK_SB.s_base + s));
                     new_path = false;
                     psec<PROF>(pf, PR_NEWPATH);
                 }
@@ -2407,39 +2452,39 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 if (path_pre<Real, EMIT, PROF>(C, P, pf, c)) {
                     finish_sample(c);
                 } else {
-                    fast_walk_begin<Real, COUNT>(S, P.o, P.d, W, cnt);
+                    fast_walk_begin<Real, COUNT>(PK_S, P.o, P.d, W, cnt);
                     walking = true;
                 }
             }
             psec<PROF>(pf, PR_RR);
             const bool was_walking = walking;
-            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF>(S, P.o, P.d, W, walking, stk, sb.min_ready,
+            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF>(PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready,
                                                                          exhausted, cnt, &pf);
             psec<PROF>(pf, PR_HIT);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)
             if (was_walking && !walking) {
-                fast_walk_resolve<Real, COUNT>(S, P.o, P.d, W, cnt);
+                fast_walk_resolve<Real, COUNT>(PK_S, P.o, P.d, W, cnt);
                 V3 c;
-                if (path_post<Real, EMIT, COUNT, PROF>(S, C, P, W.best, W.best_t, cnt, st_err, pf, c)) finish_sample(c);
+                if (path_post<Real, EMIT, COUNT, PROF>(PK_S, C, P, W.best, W.best_t, cnt, st_err, pf, c)) finish_sample(c);
             }
             psec<PROF>(pf, PR_ACC);
         } else if (slot >= 0) {
             const RtCamera& C = cam_opaque();
             prof_trip<PROF>(pf);
             if (new_path) {
-                path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(sb.s_base + s));
+                path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(PK_SB.s_base + s));
                 new_path = false;
                 psec<PROF>(pf, PR_NEWPATH);
             }
             V3 c;
-            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(S, C, P, stk, stkt, cnt, st_err, pf, c)) {
+            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(PK_S, C, P, stk, stkt, cnt, st_err, pf, c)) {
                 float4 r;
                 r.x = c.x;
                 r.y = c.y;
                 r.z = c.z;
                 r.w = __int_as_float(P.bounces);
 #ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
-                rec_store<false>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
+                rec_store<false>(PK_SB.rec + ((size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot), r);
 #endif
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;
@@ -2455,6 +2500,10 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     PixStats st;
     publish_stats(out, st, st_err, lane);
     publish_counters<COUNT, PROF>(out, cnt, pf, lane);
+#undef PK_SB
+#undef PK_REG
+#undef PK_OUT
+#undef PK_S
 }
 
 // ---------------------------------------------------------------------------
