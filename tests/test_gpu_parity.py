@@ -854,6 +854,33 @@ def test_bench_two_ranks_one_gpu_assemble_the_frame(gpu):
     assert line["n_gpus"] == 2 and line["frame_check"] is True
 
 
+@pytest.mark.parametrize("groups,scene", [(3, "cornell"), (2, "spheres")])
+def test_rccl_gather_of_tile_groups_assembles_the_frame(gpu, groups, scene):
+    """The RCCL leg on a one-GPU box (RCCL refuses two ranks on one device): a world-1
+    "nccl" process group in a child process gathers each tile group's packed u8 slab
+    (with its stats tile) through dist.gather, rt_tiles_unpack assembles the frame, and
+    frame and merged stats equal a single launch (tests/rccl_one_rank.py)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    r = subprocess.run([sys.executable, str(root / "tests" / "rccl_one_rank.py"), str(groups), scene],
+                       capture_output=True, text=True, timeout=180, env=env, cwd=str(root))
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print(out)
+    assert out["backend"] == "nccl" and out["frame_equal"] and out["stats_equal"] and out["slabs_equal_gathered"]
+    assert out["all_reduce"] == [1.5, 2.5]
+
+
 # ---------------------------------------------------------------------------
 # Adaptive sampling in rounds (rt_api.cpp launch_adaptive_rounds, pt_adapt_kernel):
 # the chunked / pool kernels render each round's samples speculatively, the adapt
