@@ -454,7 +454,11 @@ struct rt_camera {
                                        : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
             const int c_max = (v.pool || v.wpool) ? 4 : (bvh && g.lds_level == 0) ? 4 : 32;
-            const double c_target = bvh ? std::sqrt(spl) / 3.0 : spl / 8.0;
+            // (pool kernel, fixed spp, re-checked at the round-3 build: first items of spl / 64, so 4
+            // samples for the whole frame and a 1/2 share, 2 for a 1/4 share, 1 for a 1/8 share -
+            // Cornell 1/8 share 2.248 -> 2.051 ms, 1/4 3.998 -> 3.931 ms, N=1 and 1/2 unchanged;
+            // profiles/r03/sched/. Adaptive rounds keep spl / 8.)
+            const double c_target = bvh ? std::sqrt(spl) / 3.0 : (v.pool && !rounds) ? spl / 64.0 : spl / 8.0;
             int c_auto = 1;
             while (c_auto * 2 <= c_max && c_auto * 2 <= c_target) c_auto *= 2;  // pow2 floor, in [1, c_max]
             // power-of-two chunks: items are aligned to their chunk (the pool kernel derives an
