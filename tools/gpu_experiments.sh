@@ -12,6 +12,9 @@
 #   adapt_jump adaptive bench lines (reference defaults) under RT_AMD_ADAPT_JUMP arms   -> profiles/r03/exp2/
 #              (the Cornell arms of exp2 ran a variant library, RT_AMD_VARIANT=<name>, built with
 #              _build.build_native(variant=..., defines=[...]))
+#   sched_r03  rank shares N = 1..8 (SWEEP_TG) under the pool kernel's first-item chunk (Cornell) and
+#              min_ready (spheres-500), three repeats; spheres-500 tile-chunks per atomic, two repeats;
+#              adaptive Cornell (reference defaults) under first items of 1 / 2     -> profiles/r03/sched/
 # $ARMS / $CFGS override the arms and configurations (lines "name ENV=V ..." / "name bench-args").
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 R=$(pwd)
@@ -92,5 +95,20 @@ j50 RT_AMD_ADAPT_JUMP=50
 j100 RT_AMD_ADAPT_JUMP=100
 j200 RT_AMD_ADAPT_JUMP=200}" STEPS=5 bash tools/ab_env.sh || exit $?
     python tools/ab_table.py $OUT > $OUT/table.txt ;;
+  sched_r03)
+    for rep in 1 2 3; do
+      for tg in 1 2 4 8; do
+        SWEEP_TG=$tg SWEEP_VARS="RT_AMD_CHUNK=auto,2,1" timeout -k 10 120 python tools/env_sweep.py cornell >> $O/cornell_chunk.log 2>&1 || exit $?
+        SWEEP_TG=$tg SWEEP_VARS="RT_AMD_READY=auto,40" timeout -k 10 120 python tools/env_sweep.py spheres >> $O/spheres_ready.log 2>&1 || exit $?
+      done
+    done
+    for rep in 1 2; do
+      for tg in 4 8; do
+        SWEEP_TG=$tg SWEEP_VARS="RT_AMD_POOL=auto,1,4" timeout -k 10 120 python tools/env_sweep.py spheres >> $O/spheres_pool.log 2>&1 || exit $?
+      done
+    done
+    OUT=$O/adaptive CFGS="adapt --adaptive" ARMS="base
+c1 RT_AMD_CHUNK=1
+c2 RT_AMD_CHUNK=2" STEPS=5 bash tools/ab_env.sh || exit $? ;;
   *) echo "unknown experiment $1" >&2; exit 2 ;;
 esac
