@@ -47,9 +47,6 @@ SCENES = {
 KERNEL_DESC = {
     "pool": "stage-compacted pool (per-wave LDS path slots, trace/diffuse queues, in-order accumulate)",
     "chunked": "chunked (lane work pool, in-order accumulate)",
-    "wpool": "walker pool (64 BVH walkers per wave over HBM path slots, trace/shade/start queues, in-order accumulate)",
-    "wavefront": "wavefront passes (HBM path slots; per iteration a shade kernel and a walk-only kernel whose lanes "
-                 "refill from flagged slots; in-order accumulate)",
 }
 
 
@@ -349,9 +346,7 @@ def main(argv=None):
     kernel_ms = sum(a for a, _ in kt) / len(kt)
     accum_ms = sum(b for _, b in kt) / len(kt)
     kind = cam.last_kernel()  # the path kernel the library launched (rt_camera_last_kernel)
-    kernel_name = {"pool": "pt_pool_kernel", "chunked": "pt_chunk_kernel", "wpool": "pt_wpool_kernel",
-                   "wavefront": "wf_trace_kernel"}.get(
-        kind, "pt_render_kernel")
+    kernel_name = {"pool": "pt_pool_kernel", "chunked": "pt_chunk_kernel"}.get(kind, "pt_render_kernel")
 
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:

@@ -201,13 +201,12 @@ int rt_camera_pass_count(rt_camera* cam, int32_t* passes);
 
 /* Path kernel of the most recent render: RT_KERNEL_NONE before any,
  * RT_KERNEL_SEQUENTIAL (wave per 8x8 tile, adaptive sampling), RT_KERNEL_CHUNKED
- * (lane work pool + in-order accumulate), RT_KERNEL_POOL (stage-compacted
- * path pools + in-order accumulate), RT_KERNEL_WPOOL (walkers over HBM path
- * slots, BVH scenes) or RT_KERNEL_WAVEFRONT (shade / walk-only kernel iterations
- * over HBM path slots: large launches of trees walked from global memory). Diagnostics and tests; no reference
- * counterpart (the reference has one CPU loop, src/camera.ts:388-431). */
-enum { RT_KERNEL_NONE = 0, RT_KERNEL_SEQUENTIAL = 1, RT_KERNEL_CHUNKED = 2, RT_KERNEL_POOL = 3, RT_KERNEL_WPOOL = 4,
-       RT_KERNEL_WAVEFRONT = 5 };
+ * (lane work pool + in-order accumulate) or RT_KERNEL_POOL (stage-compacted
+ * path pools + in-order accumulate). Diagnostics and tests; no reference
+ * counterpart (the reference has one CPU loop, src/camera.ts:388-431).
+ * (Values 4 and 5 named the round-3 walker-pool and wavefront kernels, removed
+ * in round 4; they are not reused.) */
+enum { RT_KERNEL_NONE = 0, RT_KERNEL_SEQUENTIAL = 1, RT_KERNEL_CHUNKED = 2, RT_KERNEL_POOL = 3 };
 int rt_camera_last_kernel(rt_camera* cam, int32_t* kernel);
 
 /* Frees the camera's device resources (scene copy, frame and record buffers,

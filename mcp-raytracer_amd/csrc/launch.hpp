@@ -18,8 +18,7 @@ struct LaunchGeom {
     int my_tiles;
     int grid;
     size_t lds_bytes;  // traversal stack + the LDS-resident scene prefix
-    int lds_level;     // LDS-resident scene: 0 none, 1 traversal data + prims, 2 also mats + lights,
-                       // 3 traversal data only (walker-pool kernel)
+    int lds_level;     // LDS-resident scene: 0 none, 1 traversal data + prims, 2 also mats + lights
 };
 
 // LDS budget (stack + [tnodes][prims]) up to which the scene is copied into LDS.
@@ -39,7 +38,6 @@ struct KernelVariant {
     int trav;    // TRAV_FAST / TRAV_REFERENCE / TRAV_BRUTE (resolved, never AUTO)
     bool defer = false;  // TRAV_FAST: deferred exact sphere tests (TRAV_FAST_DEFER kernels)
     bool pool = false;   // chunked passes run the stage-compacted pool kernel (pt_pool_kernel)
-    bool wpool = false;  // chunked passes run the walker-pool kernel (pt_wpool_kernel, BVH scenes)
 };
 
 // sb == nullptr: the sequential-pixel kernel; else the chunked kernel over sb's pass.
@@ -53,12 +51,6 @@ hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut&
 // One adaptive-sampling round's accumulate / convergence pass over the pass's slots.
 hipError_t launch_adapt(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
                         const SampleBuf& sb, const AdaptRound& ar, hipStream_t stream);
-// Wavefront passes (ref precision, fast traversal): slot init, then one shade + trace
-// iteration (pt_kernel.hpp wf_shade_kernel / wf_trace_kernel).
-hipError_t launch_wf_init(const WfState& W, const SampleBuf& sb, hipStream_t stream);
-hipError_t launch_wf_iteration(bool defer, const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
-                               const SampleBuf& sb, const WfState& W, int it, int trace_grid, size_t trace_lds,
-                               hipStream_t stream);
 // Resets the stats words / counters / tile counter before a render.
 hipError_t launch_init_stats(unsigned long long* stats, unsigned long long* counters, unsigned int* tile_counter,
                              hipStream_t stream);
@@ -81,6 +73,63 @@ inline size_t stack_lds_bytes(int stack_depth, int trav, int n_prims) {
                                                            : 0;
     const size_t d = (size_t)(stack_depth > 0 ? stack_depth : 1);
     return d * kStackStride * ((trav == TRAV_FAST && kStackTnear) ? 2 * sizeof(int) : sizeof(int));
+}
+
+// The kernel template instance of a launch (one per scalar precision unit: pt_ref.hip,
+// pt_fp32.hip). sb == nullptr: the sequential-pixel kernel; else the chunked kernel, or the
+// pool kernel (product brute-force builds; RT_POOL_PROF adds its ref-precision timer build).
+template <class Real, bool EMIT, int INSTR, int TRAV, int LDSS>
+hipError_t dispatch_kernel(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
+                           const SampleBuf* sb, bool pool, hipStream_t stream) {
+    if (sb && pool) {
+        if constexpr (!EMIT && TRAV == TRAV_BRUTE && (INSTR == 0 || (RT_POOL_PROF && INSTR == 2 && sizeof(Real) == 8))) {
+            hipLaunchKernelGGL((pt_pool_kernel<Real, TRAV, LDSS>), dim3(g.grid), dim3(kBlockPool), g.lds_bytes, stream,
+                               S, reg, out, g.tiles_x, *sb);
+            return hipGetLastError();
+        } else {
+            return hipErrorInvalidValue;
+        }
+    }
+    if (sb)
+        hipLaunchKernelGGL((pt_chunk_kernel<Real, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlockChunk),
+                           g.lds_bytes, stream, S, reg, out, g.tiles_x, *sb);
+    else
+        hipLaunchKernelGGL((pt_render_kernel<Real, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
+                           stream, S, reg, out, g.tiles_x, g.my_tiles);
+    return hipGetLastError();
+}
+
+template <class Real, bool EMIT, int INSTR, int TRAV>
+hipError_t dispatch_level(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
+                          const SampleBuf* sb, bool pool, hipStream_t stream) {
+    // LDS residency levels (pt_kernel.hpp scene_prologue); never with the reference traversal
+    constexpr int L1 = trav_fast(TRAV) ? 1 : 0, L2 = TRAV == TRAV_REFERENCE ? 0 : 2;
+    if (g.lds_level >= 2) return dispatch_kernel<Real, EMIT, INSTR, TRAV, L2>(S, reg, out, g, sb, pool, stream);
+    if (g.lds_level == 1) return dispatch_kernel<Real, EMIT, INSTR, TRAV, L1>(S, reg, out, g, sb, pool, stream);
+    return dispatch_kernel<Real, EMIT, INSTR, TRAV, 0>(S, reg, out, g, sb, pool, stream);
+}
+
+template <class Real, int TRAV>
+hipError_t dispatch_variant(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
+                            const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
+    if (v.count == 2)
+        return v.emit ? dispatch_level<Real, true, 2, TRAV>(S, reg, out, g, sb, v.pool, stream)
+                      : dispatch_level<Real, false, 2, TRAV>(S, reg, out, g, sb, v.pool, stream);
+    if (v.count == 1)
+        return v.emit ? dispatch_level<Real, true, 1, TRAV>(S, reg, out, g, sb, v.pool, stream)
+                      : dispatch_level<Real, false, 1, TRAV>(S, reg, out, g, sb, v.pool, stream);
+    return v.emit ? dispatch_level<Real, true, 0, TRAV>(S, reg, out, g, sb, v.pool, stream)
+                  : dispatch_level<Real, false, 0, TRAV>(S, reg, out, g, sb, v.pool, stream);
+}
+
+template <class Real>
+hipError_t dispatch_render(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
+                           const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
+    if (v.trav == TRAV_BRUTE) return dispatch_variant<Real, TRAV_BRUTE>(v, S, reg, out, g, sb, stream);
+    if (v.trav == TRAV_FAST)
+        return v.defer ? dispatch_variant<Real, TRAV_FAST_DEFER>(v, S, reg, out, g, sb, stream)
+                       : dispatch_variant<Real, TRAV_FAST>(v, S, reg, out, g, sb, stream);
+    return dispatch_variant<Real, TRAV_REFERENCE>(v, S, reg, out, g, sb, stream);
 }
 
 }  // namespace rt

@@ -59,8 +59,6 @@ struct DevScene {
     int32_t off_tsph;                   // byte offset of tsph in the blob
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
     int32_t lds_pool_off;               // pool kernel: byte offset of the per-wave path pools (after the scene)
-    int32_t wpool_k;                    // walker-pool kernel: path slots per wave (<= 255)
-    float4* __restrict__ wslots;        // walker-pool kernel: the path slots in HBM, [wave][slot][4 groups]
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
@@ -86,6 +84,8 @@ enum {
     CT_WORDS
 };
 enum : unsigned long long { ERR_NO_BACKGROUND = 1ull, ERR_EMIT_STACK = 2ull };
+constexpr int kRecErrShift = 30;  // error flags in a sample record's bounce word (SampleBuf::err_in_rec)
+constexpr uint32_t kRecBounceMask = (1u << kRecErrShift) - 1u;
 // Diagnostic build (INSTR == 2): wave-cycles spent in each section of the path
 // loop (s_memtime, summed over waves), stored after the CT_WORDS counters.
 enum {
@@ -353,6 +353,28 @@ constexpr float kTminLo = 0.001f * (1.0f - 1e-5f);  // below the reference's tMi
 // they hold for any scene scale. Hardware rcp/sqrt (<= 1 ulp) are inside kRel.
 constexpr float kRel = 1e-5f;
 
+// The fp32 conservative filters (slab tests, sphere / planar / axis-quad pre-filters, the
+// FRay constants, the culling bound) may contract a*b+c into one FMA even in the ref TU,
+// which is compiled with -ffp-contract=off because the reference's JS arithmetic never
+// fuses. That flag must keep holding for the fp64 path and for the fp32 vector stores of
+// the exact tests, so contraction is opened per function body (RT_FP32_FUSED, a block-
+// scoped pragma: it marks only the operations written inside that block, and inlining
+// keeps the marks per operation). A filter's result reaches the output only through the
+// exact fp64 test it lets through, so the filter may round differently as long as it stays
+// conservative. Every margin below is of the form c * u * (sum of the magnitudes of the
+// terms): a fused a*b+c rounds once where the unfused form rounds twice, so each margin
+// still bounds it. The one changed form is the slab test, which no longer subtracts first
+// (see slab_t4 / FRay::eps). Before: SQ_INSTS_VALU_FMA_F32 was 0.0 % of VALU
+// on Cornell ref, 1.0 % on spheres-500 and 0.5 % on spheres-100k.
+#ifndef RT_FUSED_FILTERS
+#define RT_FUSED_FILTERS 1
+#endif
+#if RT_FUSED_FILTERS
+#define RT_FP32_FUSED _Pragma("clang fp contract(fast)")
+#else
+#define RT_FP32_FUSED
+#endif
+
 // Axis-aligned quad (scene.cpp encode_axis_quad): Plane.intersect + Quad's
 // alpha/beta test with the terms that are exact zeros dropped. Every kept
 // operation is the reference's own (a product of two fp32 values is exact in
@@ -390,6 +412,7 @@ __device__ __forceinline__ bool aquad_t_c(const RtPrim& p, V3 o3, V3 d3, Real tm
 template <int CODE>
 __device__ __forceinline__ bool aquad_maybe_v(float na, float D, float q1, float q2, float sw, float sv, float su,
                                               const float* o, const float* d, float dn, float thi, float& lo) {
+    RT_FP32_FUSED
     constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
     constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
     const float denom = na * d[a];
@@ -559,23 +582,34 @@ struct FRay {
     float o[3];
     float d[3];
     float inv[3];  // 1/d with zero components replaced by +-1e-30 (no 0*inf NaNs)
+    float noi[3];  // -(o * inv): the slab planes' t = fma(b, inv, noi)
+    float eps;     // absolute t slack of the fused slab test (>= 2u max|o * inv|, see slab_t)
     float a;       // |d|^2
     float ia;      // ~1/|d|^2
     float on;      // |o| (rounded up)
     float dn;      // |d| (rounded up)
 };
 
-
-
 __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
+    RT_FP32_FUSED
     FRay f;
     f.o[0] = o.x; f.o[1] = o.y; f.o[2] = o.z;
     f.d[0] = d.x; f.d[1] = d.y; f.d[2] = d.z;
+    float m = 0.0f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float c = f.d[a];
         const float cc = ::fabsf(c) < 1e-30f ? ::copysignf(1e-30f, c) : c;
-        f.inv[a] = 1.0f / cc;
+        f.inv[a] = __builtin_amdgcn_rcpf(cc);  // <= 1 ulp: a common factor of an axis' two planes
+        f.noi[a] = -(f.o[a] * f.inv[a]);
+        m = ::fmaxf(m, ::fabsf(f.noi[a]));
+    }
+    // 1e-6 * max|o * inv| ~ 16 u: covers the rounding of o * inv at both ends of the interval
+    f.eps = m * 1e-6f;
+    if (!(m < 1e37f)) {  // o * inv overflowed (|o| > ~1e7 with an axis-parallel d): cull nothing
+#pragma unroll
+        for (int a = 0; a < 3; ++a) f.inv[a] = f.noi[a] = 0.0f;
+        f.eps = __builtin_inff();
     }
     f.a = d.x * d.x + d.y * d.y + d.z * d.z;
     f.ia = __builtin_amdgcn_rcpf(f.a);
@@ -584,6 +618,21 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
     return f;
 }
 
+// The slab test's entry / exit parameter of the plane x_a = b: t = fma(b, inv, -o*inv), one
+// FMA instead of (b - o) * inv. The unfused form's error is relative to |t|; the fused one's
+// is absolute, |err| <= u (|o * inv| + |t|): the rounding of o * inv (FRay::noi) and the
+// final one, u = 2^-24. The acceptance test tn <= tf * 1.000002 + eps covers it: the u|t|
+// part is inside the relative 2e-6 (tn and tf are both positive whenever the box can hold a
+// hit, t > 0.001), the u|o * inv| part of either end inside eps = 1e-6 max_a |o_a inv_a|
+// (~16 u). On top of that every box is padded by 1e-6 (1 + |b|) (scene.cpp make_fast_nodes),
+// the margin the unfused test already relied on for the exact hit point.
+// A ray whose o * inv overflows gets inv = noi = 0, eps = inf: t = 0 on every plane (NaN
+// on an infinite bound, which fminf / fmaxf ignore), tf = min(thi, 0) >= 0, and the test
+// accepts every box - still the reference's hit, at brute-force cost (|o| > ~1e7 only).
+__device__ __forceinline__ float slab_t(float b, const FRay& f, int a) { return __builtin_fmaf(b, f.inv[a], f.noi[a]); }
+__device__ __forceinline__ bool slab_accept(float tn, float tf, const FRay& f) {
+    return tn <= __builtin_fmaf(tf, 1.000002f, f.eps);
+}
 
 template <class R>
 __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, float& tnear) {
@@ -591,17 +640,85 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
     float tn = kTminLo, tf = thi;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float t0 = (n.bmin[a] - f.o[a]) * f.inv[a];
-        const float t1 = (n.bmax[a] - f.o[a]) * f.inv[a];
+        const float t0 = slab_t(n.bmin[a], f, a);
+        const float t1 = slab_t(n.bmax[a], f, a);
         tn = ::fmaxf(tn, ::fminf(t0, t1));
         tf = ::fminf(tf, ::fmaxf(t0, t1));
     }
     tnear = tn;
-    return tn <= tf * 1.000002f;
+    return slab_accept(tn, tf, f);
+}
+
+// One step of the 4-wide walk (RtT4Node) at node `nd`: the slab tests of its four children,
+// the nearest hit child is returned as the next reference and the other hit children are
+// pushed farthest first (so the nearer pop first); with no hit child the next reference is
+// popped (kTravDone when the stack is empty). Branch-free:
+//  * each child's key is its entry distance's bits (a positive float orders as its bits)
+//    with the low two bits replaced by the child index, or ~0 for a miss / empty slot, so
+//    the four keys sort with a 5-exchange min/max network of u32 (10 VALU, instead of
+//    carrying (distance, reference) pairs through selects); two entry distances within
+//    4 ulps may come out in child order - that only changes the visiting order, which
+//    never changes the (t, slot) minimum the walk returns;
+//  * the references of the sorted keys are re-read from the node (its row of refs, in
+//    LDS or L1);
+//  * with n hit children the keys s1..s3 are written in the order s3, s2, s1 at stack
+//    positions sp + max(n - 1 - j, 0), so s_{n-1} .. s1 land at sp .. sp + n - 2 and the
+//    writes of missed children land at sp, overwritten or above the new top. No write
+//    goes past sp + 2: at a node of level L (root 1) the stack holds at most 3 (L - 1)
+//    entries (3 per ancestor), so writes stay below 3 t4depth <= stack_depth - 2 entries
+//    (scene.cpp: stack_depth = max(..., 3 t4depth + 1) + 1).
+template <int STRIDE>
+__device__ __forceinline__ int t4_step(const RtT4Node* nd0, const FRay& f, float thi, int* stk, int& sp) {
+    const RtT4Node* nd = reinterpret_cast<const RtT4Node*>(__builtin_assume_aligned(nd0, 16));
+    const float4 mnx = *reinterpret_cast<const float4*>(nd->bmin[0]);
+    const float4 mny = *reinterpret_cast<const float4*>(nd->bmin[1]);
+    const float4 mnz = *reinterpret_cast<const float4*>(nd->bmin[2]);
+    const float4 mxx = *reinterpret_cast<const float4*>(nd->bmax[0]);
+    const float4 mxy = *reinterpret_cast<const float4*>(nd->bmax[1]);
+    const float4 mxz = *reinterpret_cast<const float4*>(nd->bmax[2]);
+    const int4 rf = *reinterpret_cast<const int4*>(nd->ref);
+    const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w}, {mnz.x, mnz.y, mnz.z, mnz.w}};
+    const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
+    const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
+    uint32_t k[4];
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float tn = kTminLo, tf = thi;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float t0 = slab_t(bmn[a][c], f, a);
+            const float t1 = slab_t(bmx[a][c], f, a);
+            tn = ::fmaxf(tn, ::fminf(t0, t1));
+            tf = ::fminf(tf, ::fmaxf(t0, t1));
+        }
+        const bool hit = (cr[c] != kT4Empty) & slab_accept(tn, tf, f);
+        k[c] = hit ? ((__float_as_uint(tn) & ~3u) | (uint32_t)c) : ~0u;
+        n += hit ? 1 : 0;
+    }
+    auto cx = [&](int i, int j) {
+        const uint32_t lo = min(k[i], k[j]);
+        k[j] = max(k[i], k[j]);
+        k[i] = lo;
+    };
+    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+    // every read before the first write (the stack and the node may share LDS: the compiler
+    // would otherwise wait out each read before the following write)
+    const int* refs = nd->ref;
+    int rs[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rs[j] = refs[k[j] & 3u];
+    const int popped = stk[max(sp - 1, 0) * STRIDE];
+#pragma unroll
+    for (int j = 3; j >= 1; --j) stk[max(sp + n - 1 - j, sp) * STRIDE] = rs[j];
+    const int next = n > 0 ? rs[0] : (sp > 0 ? popped : kT4Empty);  // (kT4Empty = kTravDone)
+    sp = n > 0 ? sp + n - 1 : max(sp - 1, 0);
+    return next;
 }
 
 // fp32 pre-filters: false only when the exact test surely gives no t <= thi.
 __device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi, float& lo) {
+    RT_FP32_FUSED
     const float ox = f.o[0] - g.x, oy = f.o[1] - g.y, oz = f.o[2] - g.z;  // = the reference's oc
     const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
     const float r = g.w;
@@ -625,6 +742,7 @@ __device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi,
 // model), an upper bound `hi` of the t the exact test will return (+inf otherwise).
 // A surely-hit candidate's `hi` may cull the walk before its exact test runs.
 __device__ __forceinline__ bool sphere_maybe_hi(float4 g, const FRay& f, float thi, float& lo, float& hi) {
+    RT_FP32_FUSED
     const float ox = f.o[0] - g.x, oy = f.o[1] - g.y, oz = f.o[2] - g.z;
     const float b = ox * f.d[0] + oy * f.d[1] + oz * f.d[2];
     const float r = g.w;
@@ -652,6 +770,7 @@ __device__ __forceinline__ bool sphere_maybe_hi(float4 g, const FRay& f, float t
 
 template <bool QUAD>
 __device__ __forceinline__ bool planar_maybe(const RtPrim& p, const FRay& f, float thi, float& lo) {
+    RT_FP32_FUSED
     const float nx = p.g3[0], ny = p.g3[1], nz = p.g3[2];
     const float denom = nx * f.d[0] + ny * f.d[1] + nz * f.d[2];
     lo = kTminLo;
@@ -720,6 +839,7 @@ __device__ __forceinline__ bool prim_candidate(const RtPrim& p, const RayK<Real>
 
 template <class Real>
 __device__ __forceinline__ float upper_f(Real t) {
+    RT_FP32_FUSED
     // fp32 value >= t (rounded up with margin) used to cull against the best hit.
     const float x = (float)t;
     return x + ::fabsf(x) * 4e-6f + 1e-30f;
@@ -841,53 +961,8 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     // one 4-wide node step: the nearest hit child is next, the other hit
     // children are pushed farthest first (so the nearer pop first)
     auto node_step = [&](int ref) -> int {
-        const RtT4Node* nd = reinterpret_cast<const RtT4Node*>(S.tnodes) + ref;
-        const float4 mnx = *reinterpret_cast<const float4*>(nd->bmin[0]);
-        const float4 mny = *reinterpret_cast<const float4*>(nd->bmin[1]);
-        const float4 mnz = *reinterpret_cast<const float4*>(nd->bmin[2]);
-        const float4 mxx = *reinterpret_cast<const float4*>(nd->bmax[0]);
-        const float4 mxy = *reinterpret_cast<const float4*>(nd->bmax[1]);
-        const float4 mxz = *reinterpret_cast<const float4*>(nd->bmax[2]);
-        const int4 rf = *reinterpret_cast<const int4*>(nd->ref);
         if (COUNT) cnt[CT_NODE] += 4;
-        const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w}, {mnz.x, mnz.y, mnz.z, mnz.w}};
-        const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
-        const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
-        float key[4];
-        int kr[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float tn = kTminLo, tf = thi;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const float t0 = (bmn[a][c] - f.o[a]) * f.inv[a];
-                const float t1 = (bmx[a][c] - f.o[a]) * f.inv[a];
-                tn = ::fmaxf(tn, ::fminf(t0, t1));
-                tf = ::fminf(tf, ::fmaxf(t0, t1));
-            }
-            const bool hit = cr[c] != kT4Empty && tn <= tf * 1.000002f;
-            key[c] = hit ? tn : __builtin_inff();
-            kr[c] = hit ? cr[c] : kTravDone;
-        }
-        // sort (key, ref) ascending: 5 compare-exchanges
-        auto cx = [&](int i, int j) {
-            const bool sw = key[j] < key[i];
-            const float tk = sw ? key[j] : key[i];
-            key[j] = sw ? key[i] : key[j];
-            key[i] = tk;
-            const int tr = sw ? kr[j] : kr[i];
-            kr[j] = sw ? kr[i] : kr[j];
-            kr[i] = tr;
-        };
-        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-#pragma unroll
-        for (int c = 3; c >= 1; --c) {
-            if (kr[c] != kTravDone) {
-                stk[sp * kStackStride] = kr[c];
-                ++sp;
-            }
-        }
-        return kr[0] != kTravDone ? kr[0] : pop();
+        return t4_step<kStackStride>(reinterpret_cast<const RtT4Node*>(S.tnodes) + ref, f, thi, stk, sp);
     };
 #else
     // one node step: the next node / leaf to visit
@@ -1015,54 +1090,8 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             };
 #if RT_BVH4
             auto node_step = [&](int ref) -> int {
-                const RtT4Node* nd = reinterpret_cast<const RtT4Node*>(S.tnodes) + ref;
-                const float4 mnx = *reinterpret_cast<const float4*>(nd->bmin[0]);
-                const float4 mny = *reinterpret_cast<const float4*>(nd->bmin[1]);
-                const float4 mnz = *reinterpret_cast<const float4*>(nd->bmin[2]);
-                const float4 mxx = *reinterpret_cast<const float4*>(nd->bmax[0]);
-                const float4 mxy = *reinterpret_cast<const float4*>(nd->bmax[1]);
-                const float4 mxz = *reinterpret_cast<const float4*>(nd->bmax[2]);
-                const int4 rf = *reinterpret_cast<const int4*>(nd->ref);
                 if (COUNT) cnt[CT_NODE] += 4;
-                const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w},
-                                         {mnz.x, mnz.y, mnz.z, mnz.w}};
-                const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w},
-                                         {mxz.x, mxz.y, mxz.z, mxz.w}};
-                const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
-                float key[4];
-                int kr[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    float tn = kTminLo, tf = thi;
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) {
-                        const float t0 = (bmn[a][c] - f.o[a]) * f.inv[a];
-                        const float t1 = (bmx[a][c] - f.o[a]) * f.inv[a];
-                        tn = ::fmaxf(tn, ::fminf(t0, t1));
-                        tf = ::fminf(tf, ::fmaxf(t0, t1));
-                    }
-                    const bool hit = cr[c] != kT4Empty && tn <= tf * 1.000002f;
-                    key[c] = hit ? tn : __builtin_inff();
-                    kr[c] = hit ? cr[c] : kTravDone;
-                }
-                auto cx = [&](int i, int j) {
-                    const bool sw = key[j] < key[i];
-                    const float tk = sw ? key[j] : key[i];
-                    key[j] = sw ? key[i] : key[j];
-                    key[i] = tk;
-                    const int tr = sw ? kr[j] : kr[i];
-                    kr[j] = sw ? kr[i] : kr[j];
-                    kr[i] = tr;
-                };
-                cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-#pragma unroll
-                for (int c = 3; c >= 1; --c) {
-                    if (kr[c] != kTravDone) {
-                        stk[sp * STRIDE] = kr[c];
-                        ++sp;
-                    }
-                }
-                return kr[0] != kTravDone ? kr[0] : pop();
+                return t4_step<STRIDE>(reinterpret_cast<const RtT4Node*>(S.tnodes) + ref, f, thi, stk, sp);
             };
 #else
             auto node_step = [&](int ref) -> int {
@@ -1266,6 +1295,7 @@ __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Rea
 // products - fewer operations, a (slightly) wider but still conservative margin.
 template <int CODE>
 __device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, float& lo) {
+    RT_FP32_FUSED
     constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
     constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
     const float na = v[0], D = v[1], q1 = v[2], q2 = v[3], asv = v[4], asu = v[5], qm = v[6];
@@ -2033,7 +2063,7 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
         S.tsph = reinterpret_cast<const float4*>(b + S0.off_tsph);
-        if (LDSS != 3) S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);  // 3: the walk's data only
+        S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
         if (LDSS == 2) {
             S.mats = reinterpret_cast<const RtMat*>(b + S0.off_mats);
             S.lights = reinterpret_cast<const RtLight*>(b + S0.off_lights);
@@ -2046,10 +2076,9 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
 // Workgroup prologue shared by the render kernels: LDS-resident scene data
 // (one cooperative copy per workgroup) and this thread's stack columns.
 // LDSS 0: all scene reads from global memory; 1: the traversal data and the
-// primitive records in LDS; 2: also the material and light tables; 3 (walker-pool
-// kernel): the traversal data only ([tnodes][tprims][tsph]), primitive records global. (Wave-
-// uniform reads - the brute-force primitive loop, the light list - stay on
-// scalar loads from the global copy.)
+// primitive records in LDS; 2: also the material and light tables. (Wave-uniform
+// reads - the brute-force primitive loop, the light list - stay on scalar loads
+// from the global copy.)
 template <int LDSS>
 __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
     if (LDSS > 0) {
@@ -2180,6 +2209,12 @@ struct SampleBuf {
     // act == nullptr: slot a is pass tile tile0 + a / 64, lane a % 64, samples from 0.
     const int32_t* act;
     int32_t s_base;
+    // Adaptive rounds: a sample's error flags (ERR_*) travel in bits 30-31 of its record's
+    // bounce word instead of the launch's stats, so pt_adapt_kernel counts only the flags of
+    // the samples it keeps - a round renders samples past a pixel's convergence, which the
+    // reference never renders (src/camera.ts:400-425). Bounce counts stay below 2^30
+    // (loop_threshold caps depth at 1e9).
+    int32_t err_in_rec;
     int32_t s0[kMaxPhases], chunk[kMaxPhases], nch[kMaxPhases], item_base[kMaxPhases];
     double rnch[kMaxPhases];  // 1.0 / nch
 };
@@ -2206,6 +2241,16 @@ struct AdaptRound {
 // 4.78 GB for 2.62 GB of records (1.67x instead of 1.87x) at the same kernel time. The
 // chunked kernel keeps plain stores: a lane writes its item's samples in turn, and spheres-500
 // wrote 0.97 GB instead of 0.89 GB non-temporally (profiles/r02/recnt/).
+// The finished sample's error flags for its record (SampleBuf::err_in_rec): the lane's flags
+// since its previous sample (a lane runs one path at a time), which then start over; 0 and
+// the flags stay in `st_err` for the launch's stats otherwise.
+__device__ __forceinline__ int rec_err_bits(int err_in_rec, unsigned long long& st_err) {
+    if (!err_in_rec) return 0;
+    const int b = (int)((uint32_t)st_err << kRecErrShift);
+    st_err = 0;
+    return b;
+}
+
 template <bool NT>
 __device__ __forceinline__ void rec_store(float4* p, float4 r) {
     if constexpr (NT) {
@@ -2432,7 +2477,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 r.x = c.x;
                 r.y = c.y;
                 r.z = c.z;
-                r.w = __int_as_float(P.bounces);
+                r.w = __int_as_float(P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err));
                 rec_store<false>(PK_SB.rec + ((size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot), r);
                 ++s;
                 if (s < s_end) new_path = true;
@@ -2482,7 +2527,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 r.x = c.x;
                 r.y = c.y;
                 r.z = c.z;
-                r.w = __int_as_float(P.bounces);
+                r.w = __int_as_float(P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err));
 #ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
                 rec_store<false>(PK_SB.rec + ((size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot), r);
 #endif
@@ -2639,12 +2684,15 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     first_pool(sb, pool_next, pool_end, exhausted);
 
     // the sample's radiance and bounce count to its record; the slot's next phase
-    auto record = [&](V3 c, int bounces, int slot, int& s, int s_end) -> int {
+    // `err`: the sample's error flags (its miss without a background): in the record in
+    // adaptive rounds (SampleBuf::err_in_rec), else in the launch's stats
+    auto record = [&](V3 c, int bounces, int slot, int& s, int s_end, unsigned long long err = 0ull) -> int {
         float4 r;
         r.x = c.x;
         r.y = c.y;
         r.z = c.z;
-        r.w = __int_as_float(bounces);
+        r.w = __int_as_float(bounces | (sb.err_in_rec ? (int)((uint32_t)err << kRecErrShift) : 0));
+        if (!sb.err_in_rec) st_err |= err;
         rec_store<RT_REC_NT>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
         ++s;
         return s < s_end ? PH_NEW : PH_ITEM;
@@ -2781,6 +2829,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 bool term = path_pre<Real, false, PP>(C, P, pf, c);
                 V3 att;
                 int hf = 0, dmat = 0;
+                unsigned long long err = 0ull;  // this sample's error flags (its miss)
                 if (!term) {
                     const RayK<Real> ray = make_ray<Real>(P.o, P.d);
                     Real t;
@@ -2793,7 +2842,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                     psec<PP>(pf, PR_HIT);
                     if (h < 0) {
                         term = true;
-                        c = miss_color<Real, false, PP>(C, P, st_err, pf);
+                        c = miss_color<Real, false, PP>(C, P, err, pf);
                     } else {
                         V3 p, nrm, emitted, sdir;
                         bool front, planar;
@@ -2822,7 +2871,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                         }
                     }
                 }
-                phase = term ? record(c, P.bounces, slot, s, item_end(s, clog2)) : P.bounces;
+                phase = term ? record(c, P.bounces, slot, s, item_end(s, clog2), err) : P.bounces;
                 g0 = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
                                  pool_meta(phase, clog2, to_d ? dmat : 0), pool_hs(to_d ? hf : 0, s));
                 g1 = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
@@ -2857,561 +2906,5 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     publish_counters<false, PP>(out, cnt, pf, lane);
 }
 
-
-// ---------------------------------------------------------------------------
-// Walker-pool kernel (BVH scenes: fixed spp and adaptive rounds, no emission
-// stack). The chunked kernel ties a path to a lane: its resumable walk
-// (fast_walk_rounds) runs until 48 of 64 lanes are done, then those lanes shade
-// and start their next rays - so node steps ran on ~34 of 64 lanes and the
-// shading on ~30 (tools/profile_sections.py, spheres-500). Here the 64 lanes are
-// WALKERS only, and paths live in K per-wave LDS slots with three queues:
-//   T  rays ready to trace: an idle walker takes one (its o, d) and walks it;
-//   H  walks that ended: the slot holds the closest hit (prim, exact t);
-//   N  slots that start a sample (getRay) or need a work item.
-// A wave's trip is one stage: SHADE (64 hits from H: hit record, emission,
-// scatter, the mixture-PDF light sampling of a diffuse bounce, the next level's
-// depth cut-off / roulette; a finished sample is recorded and the item's next
-// sample started on the spot), START (64 slots from N), or WALK (idle walkers
-// refill from T, then the parked-leaf walk until `min_ready` walkers are idle;
-// finished walks go to H). Walk state persists in the walkers' registers across
-// SHADE / START trips. Per path the arithmetic and draw order are path_trip's
-// (shade_hit / shade_diffuse / path_pre are the functions path_post calls, the
-// walk is fast_walk_rounds), so the sample records - and the image - are
-// bit-identical to the chunked kernel's.
-// Slot (64 B, [slot][group] float4, in HBM: the wave's K slots are an 8-16 KB run
-// that stays in L2 / MALL; LDS holds only the walkers' stacks, the walk data
-// and the three u8 queues, so the kernel runs 16 waves per CU like the chunked
-// kernel): g0 {rng lo, rng hi, meta, hs}, g1 {o, pass slot}, g2 {d, T.x}, g3
-// {T.y, T.z, t (double bits, H only)}; meta = (phase + 2) | log2(item chunk) << 8
-// | (hit + 1) << 11 (H only), hs = s << 16. (An 80-byte slot with a write-only hit
-// group instead of the two read-modify-writes ran slower: 6.88 vs 6.57 ms on
-// spheres-500, profiles/r03/wpool_hbm/.) A slot is written and read by lanes
-// of one wave only; a wave's vector memory operations reach the CU's L1 and L2
-// in issue order, so a later trip's loads see an earlier trip's stores.
-// ---------------------------------------------------------------------------
-#ifndef RT_WPOOL_BLOCK
-#define RT_WPOOL_BLOCK 1024
-#endif
-constexpr int kBlockWPool = RT_WPOOL_BLOCK;
-constexpr int kWPoolSlotBytes = 64;  // four 16-byte groups (HBM)
-// LDS per wave: one entry per slot in each of the three queues
-__host__ __device__ constexpr size_t wpool_wave_bytes(int K) { return ((size_t)K * 3 + 15) / 16 * 16; }
-constexpr int kWPoolMaxK = 255;  // u8 queue entries
-
-template <class Real, int TRAV, int LDSS, bool PP = false>  // PP: section timers (INSTR == 2 launches)
-__global__ __launch_bounds__(kBlockWPool) void pt_wpool_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
-                                                                 SampleBuf sb) {
-    extern __shared__ int lds_stack[];
-    const RtCamera& C0 = S0.cam;
-    __shared__ PhaseRow ptab[kMaxPhases];
-    phase_table_init(sb, ptab);
-    const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
-    const int lane = threadIdx.x & (kWave - 1);
-    int* stk = lds_stack + threadIdx.x;  // this walker's stack column (stride kBlockWPool)
-    const int K = S0.wpool_k;
-    char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * wpool_wave_bytes(K);
-    // group q of slot k: G[4 * k + q]
-    float4* G = S0.wslots + (size_t)(blockIdx.x * (kBlockWPool / kWave) + threadIdx.x / kWave) * (size_t)K * 4;
-    uint8_t* qt = reinterpret_cast<uint8_t*>(wpool);
-    uint8_t* qh = qt + K;
-    uint8_t* qn = qh + K;
-    const int endX = min(reg.x + reg.width, C0.width);
-    const int endY = min(reg.y + reg.height, C0.height);
-    const int n_items = sb.n_items;
-    const double rtx = 1.0 / (double)tiles_x;
-    uint32_t* cnt = nullptr;  // product build: no work counters
-    unsigned long long st_err = 0;
-    __shared__ unsigned long long prof_lds[PP ? kProfWaves * kProfSlot : 1];
-    Prof pf;
-    prof_init<PP>(pf, prof_lds, lane);
-
-    for (int k = lane; k < K; k += kWave) {
-        qn[k] = (uint8_t)k;
-        G[4 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
-    }
-    int t_cnt = 0, h_cnt = 0, n_cnt = K;  // wave-uniform queue lengths (stacks)
-    int pool_next, pool_end;               // wave-uniform item hand-out
-    bool exhausted;
-    first_pool(sb, pool_next, pool_end, exhausted);
-    // the walker: the slot it walks (-1: idle), its walk state and ray
-    int wk = -1;
-    bool walking = false;
-    FastWalk<Real> W;
-    V3 wo = v3(0, 0, 0), wd = wo;
-
-    auto push = [&](uint8_t* q, int& c, bool want, int k) {
-        const unsigned long long m = __ballot(want);
-        if (want) {
-            const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            q[c + r] = (uint8_t)k;
-        }
-        c += __popcll(m);
-    };
-    // the sample's radiance and bounce count to its record; the slot's next phase
-    auto record = [&](V3 c, int bounces, int slot, int& s, int s_end) -> int {
-        float4 r;
-        r.x = c.x;
-        r.y = c.y;
-        r.z = c.z;
-        r.w = __int_as_float(bounces);
-        rec_store<RT_REC_NT>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
-        ++s;
-        return s < s_end ? PH_NEW : PH_ITEM;
-    };
-    // getRay for the slot's sample s, then the first level's cut-off / roulette; the
-    // phase after it: 0 (a ray to trace) or, when the path ended at once, recorded
-    auto start_path = [&](const RtCamera& C, Path<false>& P, int slot, int& s, int clog2) -> int {
-        int i, j;
-        slot_pixel(sb, reg, tiles_x, rtx, endX, endY, slot, i, j);
-        path_begin<Real, false>(C, P, pixel_center<Real>(C, i, j), (uint32_t)j * (uint32_t)C.width + (uint32_t)i,
-                                (uint32_t)(sb.s_base + s));
-        V3 c;
-        if (path_pre<Real, false, false>(C, P, pf, c)) return record(c, P.bounces, slot, s, item_end(s, clog2));
-        return 0;
-    };
-    auto store = [&](int k, const Path<false>& P, int phase, int clog2, int slot, int s) {
-        G[4 * k] = make_float4(__uint_as_float((uint32_t)P.rng), __uint_as_float((uint32_t)(P.rng >> 32)),
-                           pool_meta(phase, clog2, 0), pool_hs(0, s));
-        G[4 * k + 1] = make_float4(P.o.x, P.o.y, P.o.z, __int_as_float(slot));
-        G[4 * k + 2] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
-        G[4 * k + 3] = make_float4(P.T.y, P.T.z, 0.f, 0.f);
-    };
-
-    while (true) {
-        // other lanes' slot and queue writes of the previous trip (one wave: LDS is in order)
-        __asm__ volatile("" ::: "memory");
-        const int nwalk = __popcll(__ballot(wk >= 0));
-        if (t_cnt + h_cnt + n_cnt + nwalk == 0) break;
-        // the stage of this trip (wave-uniform): full SHADE / START trips first, else walk
-        // while there are rays, else whatever is left
-        const int stage = h_cnt >= kWave ? 1 : n_cnt >= kWave ? 2 : (t_cnt > 0 || nwalk > 0) ? 0 : h_cnt > 0 ? 1 : 2;
-        prof_trip<PP>(pf);
-        psec<PP>(pf, PR_ACC);  // the previous trip's queue appends and stage choice
-        if (stage == 0) {
-            // ---- WALK: idle walkers take rays from T, then walk ----
-            const unsigned long long idle = __ballot(wk < 0);
-            const int m = min(__popcll(idle), t_cnt);
-            if (m > 0) {
-                const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                if (wk < 0 && r < m) {
-                    const int k = (int)qt[t_cnt - m + r];
-                    const float4 g1 = G[4 * k + 1], g2 = G[4 * k + 2];
-                    wo = V3{g1.x, g1.y, g1.z};
-                    wd = V3{g2.x, g2.y, g2.z};
-                    wk = k;
-                    fast_walk_begin<Real, false>(S, wo, wd, W, cnt);
-                    walking = true;
-                }
-                t_cnt -= m;
-            }
-            psec<PP>(pf, PR_RR);  // refill (lanes: the walkers that took a ray)
-            fast_walk_rounds<Real, false, TRAV == TRAV_FAST_DEFER, PP, kBlockWPool>(S, wo, wd, W, walking, stk,
-                                                                                    sb.min_ready, false, cnt, &pf);
-            psec<PP>(pf, PR_HIT);
-            const bool fin = wk >= 0 && !walking;
-            if (fin) {
-                fast_walk_resolve<Real, false>(S, wo, wd, W, cnt);
-                float tz, tw;
-                if (sizeof(Real) == 8) {
-                    const unsigned long long tb = (unsigned long long)__double_as_longlong((double)W.best_t);
-                    tz = __uint_as_float((uint32_t)tb);
-                    tw = __uint_as_float((uint32_t)(tb >> 32));
-                } else {
-                    tz = (float)W.best_t;
-                    tw = 0.f;
-                }
-                const float4 g0 = G[4 * wk];
-                G[4 * wk] = make_float4(g0.x, g0.y, pool_meta(meta_phase(g0.z), meta_clog2(g0.z), W.best + 1), g0.w);
-                const float4 g3 = G[4 * wk + 3];
-                G[4 * wk + 3] = make_float4(g3.x, g3.y, tz, tw);
-            }
-            push(qh, h_cnt, fin, wk);
-            if (fin) wk = -1;
-            psec<PP>(pf, PR_MISS);  // finished walks to H (lanes: those walks)
-        } else if (stage == 1) {
-            // ---- SHADE: up to 64 walked rays ----
-            const int n = min(kWave, h_cnt);
-            int k = -1;
-            if (lane < n) k = (int)qh[h_cnt - n + lane];
-            h_cnt -= n;
-            int phase = PH_ITEM;
-            if (k >= 0) {
-                const float4 g0 = G[4 * k], g1 = G[4 * k + 1], g2 = G[4 * k + 2], g3 = G[4 * k + 3];
-                Path<false> P;
-                P.rng = (uint64_t)__float_as_uint(g0.x) | ((uint64_t)__float_as_uint(g0.y) << 32);
-                P.bounces = meta_phase(g0.z);
-                P.em_n = 0;
-                P.o = V3{g1.x, g1.y, g1.z};
-                P.d = V3{g2.x, g2.y, g2.z};
-                P.T = V3{g2.w, g3.x, g3.y};
-                const int clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w), h = (int)(__float_as_uint(g0.z) >> 11) - 1;
-                int s = hs_s(g0.w);
-                Real t;
-                if (sizeof(Real) == 8)
-                    t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(g3.z) |
-                                                               ((unsigned long long)__float_as_uint(g3.w) << 32)));
-                else
-                    t = (Real)g3.z;
-                const RtCamera& C = cam_opaque();
-                V3 c;
-                bool term = false;
-                psec<PP>(pf, PR_TILE);  // SHADE: slot loads
-                if (h < 0) {
-                    term = true;
-                    c = miss_color<Real, false, PP>(C, P, st_err, pf);
-                } else {
-                    V3 p, nrm, emitted, att, sdir;
-                    bool front, planar;
-                    const int kind = shade_hit<Real, false, false, PP>(S, P, h, t, cnt, pf, p, nrm, front, planar,
-                                                                      emitted, att, sdir);
-                    if (kind == SC_NONE) {
-                        term = true;
-                        c = emitted;
-                    } else {
-                        ++P.bounces;
-                        if (kind == SC_SPEC) {
-                            P.T = mulv(P.T, att);
-                            P.o = p;
-                            P.d = sdir;
-                        } else if (shade_diffuse<Real, false, false, PP>(S, C, P, h, planar, front, p, nrm, att, cnt,
-                                                                         pf)) {
-                            term = true;
-                            c = emitted;
-                        }
-                    }
-                }
-                if (!term) term = path_pre<Real, false, false>(C, P, pf, c);  // the next level's cut-off / roulette
-                phase = P.bounces;
-                if (term) {
-                    phase = record(c, P.bounces, slot, s, item_end(s, clog2));
-                    if (phase == PH_NEW) phase = start_path(C, P, slot, s, clog2);  // the item's next sample
-                }
-                store(k, P, phase, clog2, slot, s);
-            }
-            push(qt, t_cnt, k >= 0 && phase >= 0, k);
-            push(qn, n_cnt, k >= 0 && phase < 0, k);
-            psec<PP>(pf, PR_ACC);
-        } else {
-            // ---- START: up to 64 slots that begin a sample or need a work item ----
-            const int n = min(kWave, n_cnt);
-            int k = -1;
-            if (lane < n) k = (int)qn[n_cnt - n + lane];
-            n_cnt -= n;
-            float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f), g1 = g0;
-            if (k >= 0) {
-                g0 = G[4 * k];
-                g1 = G[4 * k + 1];
-            }
-            int phase = meta_phase(g0.z), clog2 = meta_clog2(g0.z), slot = __float_as_int(g1.w);
-            int s = hs_s(g0.w);
-            // work items for slots without one (the chunked kernel's guided hand-out)
-            const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
-            if (need != 0ull && !exhausted) {
-                if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
-                if (!exhausted) {
-                    const int take = min(__popcll(need), pool_end - pool_next);
-                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                    if (k >= 0 && phase == PH_ITEM && rank < take) {
-                        int tl, l, s1, e1, i, j;
-                        item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
-                        if (slot_pixel(sb, reg, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
-                            slot = tl * 64 + l;
-                            s = s1;
-                            clog2 = __builtin_ctz((uint32_t)(e1 - s1));  // power-of-two, aligned chunks
-                            phase = PH_NEW;
-                        }
-                    }
-                    pool_next += take;
-                }
-            }
-            const bool keep = k >= 0 && (phase != PH_ITEM || !exhausted);  // drained slots leave the pool
-            if (k >= 0 && phase == PH_NEW) {
-                Path<false> P;
-                phase = start_path(cam_opaque(), P, slot, s, clog2);
-                store(k, P, phase, clog2, slot, s);
-            } else if (keep) {
-                G[4 * k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);  // still waiting for a work item
-            }
-            push(qt, t_cnt, keep && phase >= 0, k);
-            push(qn, n_cnt, keep && phase < 0, k);
-            psec<PP>(pf, PR_NEWPATH);  // START (hand-out and path starts)
-        }
-    }
-    PixStats st;
-    publish_stats(out, st, st_err, lane);
-    publish_counters<false, PP>(out, cnt, pf, lane);
-}
-
-
-// ---------------------------------------------------------------------------
-// Wavefront passes for large BVH launches (trees walked from global memory,
-// e.g. spheres-100k / BASELINE config 5). In the chunked kernel a lane owns a
-// path through its whole walk; the walk is ~83 % of the time, bound by the
-// dependent node fetches of lanes that are mostly idle (node steps on ~27 of 64
-// lanes) at 4 waves per SIMD, because the shading code's registers cap the
-// occupancy. Here the pass's paths live in WfState's HBM slots and every
-// iteration runs two kernels:
-//   wf_shade_kernel (one lane per slot): the rest of the level of the ray traced
-//     last iteration (path_post: miss, emission, scatter, mixture-PDF light
-//     sampling), the sample record when the path ends, the item hand-out and the
-//     next sample's getRay (path_begin), and the next level's depth cut-off /
-//     roulette (path_pre); it flags the slots that have a ray to trace;
-//   wf_trace_kernel (walk only, <= 96 VGPRs, 5 waves per SIMD): each wave owns a
-//     contiguous run of slots; idle lanes take the next flagged slots (ballot +
-//     rank compaction through LDS) and walk them (fast_walk_rounds); a walk that
-//     ends writes (hit, exact t) to its slot and the lane takes the next ray.
-// Per path, the arithmetic, the draw order and the sample record are the
-// chunked kernel's (the same path_begin / path_pre / path_post, the same walk),
-// so the image is bit-identical; the accumulate pass is unchanged.
-// ---------------------------------------------------------------------------
-struct WfState {
-    float4* s0;            // {o, d.x}
-    float4* s1;            // {d.y, d.z, T.x, T.y}
-    float4* s2;            // {T.z, rng lo, rng hi, -}
-    int4* s3;              // {pass slot, s, s_end, phase}: phase = bounces (a ray in flight), PH_NEW, PH_ITEM
-    float4* hit;           // {t lo, t hi, prim + 1, -} (t: the Real's bits)
-    uint8_t* flag;         // 1: the slot's ray is to be traced this iteration
-    int2* wpool;           // per shade wave: its item range {pool_next, pool_end}; pool_next = INT_MAX: exhausted
-    unsigned int* traced;  // per iteration: 1 when the trace kernel walked any ray
-    unsigned long long* live;  // per shade wave: its slots with a ray in flight (ballot); 0 + exhausted: skip
-    int32_t n;             // slots
-    int32_t per_wave;      // trace kernel: slots per wave (a multiple of 64)
-};
-constexpr int kBlockWf = 256;
-// The path state streams through HBM once per iteration: non-temporal loads and stores,
-// so it does not evict the BVH (the walk's working set) from the L2 between iterations.
-__device__ __forceinline__ float4 nt_ld(const float4* p) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ int4 nt_ld(const int4* p) {
-    const float4 v = nt_ld(reinterpret_cast<const float4*>(p));
-    return make_int4(__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w));
-}
-__device__ __forceinline__ void nt_st(float4* p, float4 v) { rec_store<true>(p, v); }
-__device__ __forceinline__ void nt_st(int4* p, int4 v) {
-    rec_store<true>(reinterpret_cast<float4*>(p),
-                    make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w)));
-}
-#ifndef RT_WF_WAVES
-#define RT_WF_WAVES 5  // trace kernel: waves per SIMD (launch bound: <= 96 VGPRs)
-#endif
-constexpr int kWfWavesPerSimd = RT_WF_WAVES;
-
-template <class Real>  // (a template: the header is in several units)
-__global__ __launch_bounds__(kBlockWf) void wf_init_kernel(WfState W, SampleBuf sb) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < W.n) {
-        W.s3[p] = make_int4(0, 0, 0, PH_ITEM);
-        W.flag[p] = 0;
-    }
-    if (p < (W.n + kWave - 1) / kWave) W.live[p] = 0ull;
-    const int w = p;  // shade wave w's static first pool (first_pool, per shade wave)
-    if (w < (W.n + kWave - 1) / kWave) {
-        const long a = (long)w * sb.pool;
-        W.wpool[w] = a < sb.n_items ? make_int2((int)a, (int)min(a + sb.pool, (long)sb.n_items))
-                                    : make_int2(0x7fffffff, 0x7fffffff);
-    }
-}
-
-template <class Real>
-__global__ __launch_bounds__(kBlockWf) void wf_shade_kernel(DevScene S, RtRegion reg, RenderOut out, int tiles_x,
-                                                            SampleBuf sb, WfState W, int it) {
-    if (it > 0 && W.traced[it - 1] == 0u) return;  // the pass ended an iteration ago
-    __shared__ PhaseRow ptab[kMaxPhases];
-    phase_table_init(sb, ptab);
-    const int lane = threadIdx.x & (kWave - 1);
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const int wave = p / kWave;
-    const bool valid = p < W.n;
-    // a wave whose slots are all idle once the items are exhausted is done for the pass
-    if (valid && W.live[wave] == 0ull && W.wpool[wave].x == 0x7fffffff) return;
-    const RtCamera& C0 = S.cam;
-    const int endX = min(reg.x + reg.width, C0.width);
-    const int endY = min(reg.y + reg.height, C0.height);
-    const double rtx = 1.0 / (double)tiles_x;
-    unsigned long long st_err = 0;
-    Prof pf;
-    int4 q = valid ? nt_ld(W.s3 + p) : make_int4(0, 0, 0, PH_ITEM);
-    int slot = q.x, s = q.y, s_end = q.z, phase = q.w;
-    Path<false> P;
-    P.em_n = 0;
-    bool ray = false;
-    auto record = [&](V3 c) {
-        float4 r;
-        r.x = c.x;
-        r.y = c.y;
-        r.z = c.z;
-        r.w = __int_as_float(P.bounces);
-        rec_store<true>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
-        ++s;
-        phase = s < s_end ? PH_NEW : PH_ITEM;
-    };
-    const RtCamera& C = cam_opaque();
-    if (valid && phase >= 0) {  // the ray traced last iteration: the rest of its level
-        const float4 a = nt_ld(W.s0 + p), b = nt_ld(W.s1 + p), c2 = nt_ld(W.s2 + p), h = nt_ld(W.hit + p);
-        P.o = V3{a.x, a.y, a.z};
-        P.d = V3{a.w, b.x, b.y};
-        P.T = V3{b.z, b.w, c2.x};
-        P.rng = (uint64_t)__float_as_uint(c2.y) | ((uint64_t)__float_as_uint(c2.z) << 32);
-        P.bounces = phase;
-        Real t;
-        if (sizeof(Real) == 8)
-            t = (Real)__longlong_as_double((long long)((unsigned long long)__float_as_uint(h.x) |
-                                                       ((unsigned long long)__float_as_uint(h.y) << 32)));
-        else
-            t = (Real)h.x;
-        V3 c;
-        if (path_post<Real, false, false, false>(S, C, P, __float_as_int(h.z) - 1, t, nullptr, st_err, pf, c)) record(c);
-        else if (path_pre<Real, false, false>(C, P, pf, c)) record(c);
-        else ray = true;
-    }
-    // item hand-out (the chunked kernel's guided schedule, per shade wave) and path starts,
-    // until every lane has a ray or no work is left
-    int2 wp = W.wpool[min(wave, (W.n - 1) / kWave)];
-    int pool_next = __builtin_amdgcn_readfirstlane(wp.x), pool_end = __builtin_amdgcn_readfirstlane(wp.y);
-    bool exhausted = pool_next == 0x7fffffff;
-    while (true) {
-        const unsigned long long need = __ballot(valid && !ray && phase == PH_ITEM);
-        if (need != 0ull && !exhausted) {
-            if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
-            if (!exhausted) {
-                const int take = min(__popcll(need), pool_end - pool_next);
-                const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                if (valid && !ray && phase == PH_ITEM && rank < take) {
-                    int tl, l, s1, e1, i, j;
-                    item_decode(sb, ptab, pool_next + rank, tl, l, s1, e1);
-                    if (slot_pixel(sb, reg, tiles_x, rtx, endX, endY, tl * 64 + l, i, j)) {
-                        slot = tl * 64 + l;
-                        s = s1;
-                        s_end = e1;
-                        phase = PH_NEW;
-                    }
-                }
-                pool_next += take;
-            }
-        }
-        const bool start = valid && !ray && phase == PH_NEW;
-        if (__ballot(start) == 0ull) {
-            if (need == 0ull || exhausted) break;
-            continue;  // items consumed without a pixel (outside the region): hand out more
-        }
-        if (start) {
-            int i, j;
-            slot_pixel(sb, reg, tiles_x, rtx, endX, endY, slot, i, j);
-            path_begin<Real, false>(C, P, pixel_center<Real>(C, i, j), (uint32_t)j * (uint32_t)C.width + (uint32_t)i,
-                                    (uint32_t)(sb.s_base + s));
-            V3 c;
-            if (path_pre<Real, false, false>(C, P, pf, c)) record(c);
-            else ray = true;
-        }
-    }
-    if (valid) {
-        if (ray) {
-            phase = P.bounces;
-            nt_st(W.s0 + p, make_float4(P.o.x, P.o.y, P.o.z, P.d.x));
-            nt_st(W.s1 + p, make_float4(P.d.y, P.d.z, P.T.x, P.T.y));
-            nt_st(W.s2 + p, make_float4(P.T.z, __uint_as_float((uint32_t)P.rng),
-                                        __uint_as_float((uint32_t)(P.rng >> 32)), 0.f));
-        }
-        nt_st(W.s3 + p, make_int4(slot, s, s_end, phase));
-        W.flag[p] = ray ? 1 : 0;
-    }
-    const unsigned long long live = __ballot(valid && ray);
-    if (valid && lane == 0) {
-        W.wpool[wave] = make_int2(exhausted ? 0x7fffffff : pool_next, exhausted ? 0x7fffffff : pool_end);
-        W.live[wave] = live;
-    }
-    const unsigned long long err = wave_or(st_err);
-    if (lane == 0 && err) atomicOr(&out.stats[ST_ERROR * kStatStride], err);
-}
-
-template <class Real, int TRAV>
-__global__ __launch_bounds__(kBlockWf, kWfWavesPerSimd) void wf_trace_kernel(DevScene S, WfState W, SampleBuf sb,
-                                                                              int it) {
-    if (it > 0 && W.traced[it - 1] == 0u) return;
-    extern __shared__ int lds_stack[];
-    __shared__ int xfer[kBlockWf / kWave][kWave];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    int* stk = lds_stack + threadIdx.x;  // this lane's stack column (stride kBlockWf)
-    const int gw = blockIdx.x * (kBlockWf / kWave) + wv;
-    const long b0 = (long)gw * W.per_wave;
-    const int end = (int)min(b0 + W.per_wave, (long)W.n);  // per_wave and n are multiples of 256
-    int win = (int)min(b0, (long)W.n);  // the scan window [win, win + 256): one flag word (4 slots) per lane
-    bool have = win < end;
-    // the window's flagged slots not taken yet, by sub-window q: slot win + 4 * lane + q
-    unsigned long long rem[4] = {0ull, 0ull, 0ull, 0ull};
-    const uint32_t* fw = reinterpret_cast<const uint32_t*>(W.flag);
-    auto load_window = [&]() {
-        const int x = win + 4 * lane;
-        const uint32_t word = x < end ? fw[x >> 2] : 0u;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rem[q] = __ballot(((word >> (8 * q)) & 0xffu) != 0u);
-    };
-    if (have) load_window();
-    int slot = -1;
-    bool walking = false, any = false;
-    FastWalk<Real> Wk;
-    V3 o = v3(0, 0, 0), d = o;
-    while (true) {
-        // idle lanes take the window's next flagged slots (ballot ranks through LDS)
-        while (have) {
-            const unsigned long long idle = __ballot(slot < 0);
-            const int n_idle = __popcll(idle);
-            if (n_idle == 0 || (n_idle < sb.refill_min && __ballot(walking) != 0ull)) break;
-            const int q = rem[0] ? 0 : rem[1] ? 1 : rem[2] ? 2 : rem[3] ? 3 : 4;
-            if (q == 4) {
-                win += 4 * kWave;
-                have = win < end;
-                if (have) load_window();
-                continue;
-            }
-            const unsigned long long m = rem[0] ? rem[0] : rem[1] ? rem[1] : rem[2] ? rem[2] : rem[3];
-            const bool act = (m >> lane) & 1ull;
-            const int take = min(__popcll(m), n_idle);
-            const int ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (act && ra < take) xfer[wv][ra] = win + 4 * lane + q;
-            const unsigned long long taken = __ballot(act && ra < take);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k == q) rem[k] &= ~taken;
-            __asm__ volatile("" ::: "memory");  // the xfer writes before the reads (one wave: LDS in order)
-            const int ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            if (slot < 0 && ri < take) {
-                slot = xfer[wv][ri];
-                const float4 a = nt_ld(W.s0 + slot), b = nt_ld(W.s1 + slot);
-                o = V3{a.x, a.y, a.z};
-                d = V3{a.w, b.x, b.y};
-                fast_walk_begin<Real, false>(S, o, d, Wk, nullptr);
-                walking = true;
-                any = true;
-            }
-            __asm__ volatile("" ::: "memory");
-        }
-        const int next = have ? win : end;  // (scan state for the drain decision below)
-        if (__ballot(walking) == 0ull && next >= end) break;
-        fast_walk_rounds<Real, false, TRAV == TRAV_FAST_DEFER, false, kBlockWf>(S, o, d, Wk, walking, stk,
-                                                                               sb.min_ready, next >= end, nullptr);
-        if (slot >= 0 && !walking) {
-            fast_walk_resolve<Real, false>(S, o, d, Wk, nullptr);
-            float tx, ty;
-            if (sizeof(Real) == 8) {
-                const unsigned long long tb = (unsigned long long)__double_as_longlong((double)Wk.best_t);
-                tx = __uint_as_float((uint32_t)tb);
-                ty = __uint_as_float((uint32_t)(tb >> 32));
-            } else {
-                tx = (float)Wk.best_t;
-                ty = 0.f;
-            }
-            nt_st(W.hit + slot, make_float4(tx, ty, __int_as_float(Wk.best + 1), 0.f));
-            slot = -1;
-        }
-    }
-    if (__ballot(any) != 0ull && lane == 0) W.traced[it] = 1u;
-}
 
 }  // namespace rt

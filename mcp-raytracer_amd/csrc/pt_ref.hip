@@ -5,65 +5,9 @@
 
 namespace rt {
 
-template <bool EMIT, int INSTR, int TRAV, int LDSS>
-static hipError_t go2(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
-                      const SampleBuf* sb, int pk, hipStream_t stream) {
-    if (sb && pk == 2) {  // walker-pool kernel: product BVH builds
-        if constexpr (!EMIT && INSTR != 1 && trav_fast(TRAV) && (LDSS == 0 || LDSS == 3)) {
-            hipLaunchKernelGGL((pt_wpool_kernel<double, TRAV, LDSS, INSTR == 2>), dim3(g.grid), dim3(kBlockWPool), g.lds_bytes,
-                               stream, S, reg, out, g.tiles_x, *sb);
-            return hipGetLastError();
-        } else {
-            return hipErrorInvalidValue;
-        }
-    }
-    if constexpr (LDSS == 3) return hipErrorInvalidValue;  // the walker-pool kernel's level only
-    if (sb && pk == 1) {  // stage-compacted pool kernel: product brute-force builds only
-        if constexpr (!EMIT && (INSTR == 0 || (RT_POOL_PROF && INSTR == 2)) && TRAV == TRAV_BRUTE) {
-            hipLaunchKernelGGL((pt_pool_kernel<double, TRAV, LDSS>), dim3(g.grid), dim3(kBlockPool), g.lds_bytes, stream,
-                               S, reg, out, g.tiles_x, *sb);
-            return hipGetLastError();
-        } else {
-            return hipErrorInvalidValue;
-        }
-    }
-    if (sb)
-        hipLaunchKernelGGL((pt_chunk_kernel<double, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlockChunk), g.lds_bytes,
-                           stream, S, reg, out, g.tiles_x, *sb);
-    else
-        hipLaunchKernelGGL((pt_render_kernel<double, EMIT, INSTR, TRAV, LDSS>), dim3(g.grid), dim3(kBlock), g.lds_bytes,
-                           stream, S, reg, out, g.tiles_x, g.my_tiles);
-    return hipGetLastError();
-}
-
-template <bool EMIT, int INSTR, int TRAV>
-static hipError_t go(const DevScene& S, const RtRegion& reg, const RenderOut& out, const LaunchGeom& g,
-                     const SampleBuf* sb, int pk, hipStream_t stream) {
-    // LDS residency levels (pt_kernel.hpp scene_prologue); never with the reference traversal
-    constexpr int L1 = trav_fast(TRAV) ? 1 : 0, L2 = TRAV == TRAV_REFERENCE ? 0 : 2;
-    if (g.lds_level == 3) {  // the walker-pool kernel's walk-data-only level
-        if constexpr (trav_fast(TRAV)) return go2<EMIT, INSTR, TRAV, 3>(S, reg, out, g, sb, pk, stream);
-        else return hipErrorInvalidValue;
-    }
-    if (g.lds_level >= 2) return go2<EMIT, INSTR, TRAV, L2>(S, reg, out, g, sb, pk, stream);
-    if (g.lds_level == 1) return go2<EMIT, INSTR, TRAV, L1>(S, reg, out, g, sb, pk, stream);
-    return go2<EMIT, INSTR, TRAV, 0>(S, reg, out, g, sb, pk, stream);
-}
-
-template <int TRAV>
-static hipError_t go_t(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
-                       const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
-    if (v.count == 2) return v.emit ? go<true, 2, TRAV>(S, reg, out, g, sb, v.wpool ? 2 : v.pool ? 1 : 0, stream) : go<false, 2, TRAV>(S, reg, out, g, sb, v.wpool ? 2 : v.pool ? 1 : 0, stream);
-    if (v.count == 1) return v.emit ? go<true, 1, TRAV>(S, reg, out, g, sb, v.wpool ? 2 : v.pool ? 1 : 0, stream) : go<false, 1, TRAV>(S, reg, out, g, sb, v.wpool ? 2 : v.pool ? 1 : 0, stream);
-    return v.emit ? go<true, 0, TRAV>(S, reg, out, g, sb, v.wpool ? 2 : v.pool ? 1 : 0, stream) : go<false, 0, TRAV>(S, reg, out, g, sb, v.wpool ? 2 : v.pool ? 1 : 0, stream);
-}
-
 hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
                              const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
-    if (v.trav == TRAV_BRUTE) return go_t<TRAV_BRUTE>(v, S, reg, out, g, sb, stream);
-    if (v.trav == TRAV_FAST)
-        return v.defer ? go_t<TRAV_FAST_DEFER>(v, S, reg, out, g, sb, stream) : go_t<TRAV_FAST>(v, S, reg, out, g, sb, stream);
-    return go_t<TRAV_REFERENCE>(v, S, reg, out, g, sb, stream);
+    return dispatch_render<double>(v, S, reg, out, g, sb, stream);
 }
 
 __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long* counters,
@@ -166,6 +110,7 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
     const double rtx = 1.0 / (double)tiles_x;
     const int endX = min(reg.x + reg.width, C.width), endY = min(reg.y + reg.height, C.height);
     PixStats st;
+    unsigned long long st_err = 0;
     __shared__ unsigned int wcnt[kAccBlock / kWave];
     __shared__ unsigned int wbase;
     const int stride = gridDim.x * blockDim.x;
@@ -181,6 +126,7 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
             int n = 0, bmin = 0x7fffffff, bmax = 0;
             unsigned long long bsum = 0;
             double sIll = 0.0, sIll2 = 0.0;
+            unsigned long long err = 0;  // error flags of the samples kept (SampleBuf::err_in_rec)
             if (sb.s_base > 0) {
                 const AdaptPix q = ar.state[ls];
                 color = v3(q.c.x, q.c.y, q.c.z);
@@ -199,7 +145,9 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
                 const V3 c = v3(r.x, r.y, r.z);
                 color = add(color, c);
                 ++n;
-                const int b = __float_as_int(r.w);
+                const uint32_t bw = __float_as_uint(r.w);
+                const int b = (int)(bw & kRecBounceMask);
+                err |= (unsigned long long)(bw >> kRecErrShift);
                 bsum += (unsigned long long)b;
                 bmin = min(bmin, b);
                 bmax = max(bmax, b);
@@ -208,6 +156,7 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
                 sIll2 += il * il;
                 done = n >= C.n_samples || pixel_converged(C, n, sIll, sIll2);
             }
+            st_err |= err;
             if (done) {
                 const uint32_t opix = out.packed ? (uint32_t)ls : (uint32_t)j * (uint32_t)C.width + (uint32_t)i;
                 finish_pixel(C, out, opix, color, n, bsum, bmin, bmax, st);
@@ -240,15 +189,15 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
         }
         __syncthreads();
     }
-    __shared__ unsigned long long red[kAccBlock / kWave][7];
-    const unsigned long long v[7] = {wave_sum(st.pixels), wave_sum(st.samples), wave_min(st.smin), wave_max(st.smax),
-                                     wave_sum(st.b),      wave_min(st.bmin),    wave_max(st.bmax)};
+    __shared__ unsigned long long red[kAccBlock / kWave][8];
+    const unsigned long long v[8] = {wave_sum(st.pixels), wave_sum(st.samples), wave_min(st.smin), wave_max(st.smax),
+                                     wave_sum(st.b),      wave_min(st.bmin),    wave_max(st.bmax), wave_or(st_err)};
     if (lane == 0)
-        for (int q = 0; q < 7; ++q) red[w][q] = v[q];
+        for (int q = 0; q < 8; ++q) red[w][q] = v[q];
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long t[7];
-        for (int q = 0; q < 7; ++q) t[q] = red[0][q];
+        unsigned long long t[8];
+        for (int q = 0; q < 8; ++q) t[q] = red[0][q];
         for (int u = 1; u < kAccBlock / kWave; ++u) {
             t[0] += red[u][0];
             t[1] += red[u][1];
@@ -257,8 +206,9 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
             t[4] += red[u][4];
             t[5] = min(t[5], red[u][5]);
             t[6] = max(t[6], red[u][6]);
+            t[7] |= red[u][7];
         }
-        stats_atomics(out, t[0], t[1], t[2], t[3], t[4], t[5], t[6], 0ull);
+        stats_atomics(out, t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7]);
     }
 }
 
@@ -274,28 +224,6 @@ hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut&
     // about two blocks' worth of slots per thread-slot of the chip: 2 x 256 CUs x 1024 threads
     const int grid = std::max(1, std::min((sb.slots + kAccBlock - 1) / kAccBlock, 2 * 256 * 1024 / kAccBlock));
     hipLaunchKernelGGL(pt_accum_kernel, dim3(grid), dim3(kAccBlock), 0, stream, S, reg, out, tiles_x, sb);
-    return hipGetLastError();
-}
-
-// Wavefront passes (pt_kernel.hpp WfState): init, then per iteration shade + trace.
-hipError_t launch_wf_init(const WfState& W, const SampleBuf& sb, hipStream_t stream) {
-    const int n = std::max(W.n, (W.n + kWave - 1) / kWave);
-    hipLaunchKernelGGL(wf_init_kernel<double>, dim3((n + kBlockWf - 1) / kBlockWf), dim3(kBlockWf), 0, stream, W, sb);
-    return hipGetLastError();
-}
-hipError_t launch_wf_iteration(bool defer, const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
-                               const SampleBuf& sb, const WfState& W, int it, int trace_grid, size_t trace_lds,
-                               hipStream_t stream) {
-    hipLaunchKernelGGL(wf_shade_kernel<double>, dim3((W.n + kBlockWf - 1) / kBlockWf), dim3(kBlockWf), 0, stream, S,
-                       reg, out, tiles_x, sb, W, it);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (defer)
-        hipLaunchKernelGGL((wf_trace_kernel<double, TRAV_FAST_DEFER>), dim3(trace_grid), dim3(kBlockWf), trace_lds,
-                           stream, S, W, sb, it);
-    else
-        hipLaunchKernelGGL((wf_trace_kernel<double, TRAV_FAST>), dim3(trace_grid), dim3(kBlockWf), trace_lds, stream,
-                           S, W, sb, it);
     return hipGetLastError();
 }
 

@@ -146,7 +146,7 @@ struct rt_camera {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         for (void* p : {(void*)d_blob, (void*)d_stats, (void*)d_counters, (void*)d_tile, (void*)d_rgb, (void*)d_rad,
-                        (void*)d_sbuf, (void*)d_wslots})
+                        (void*)d_sbuf})
             if (p) (void)hipFree(p);
         // every freed pointer is reset: a later ensure_device / ensure_frame /
         // ensure_sbuf (possibly on another device) must reallocate all of them
@@ -158,9 +158,6 @@ struct rt_camera {
         d_rad = nullptr;
         d_sbuf = nullptr;
         sbuf_cap = 0;
-        d_wslots = nullptr;
-        wslots_cap = 0;
-        free_wf();
         free_adapt_buffers();
         if (d_acount) (void)hipFree(d_acount);
         d_acount = nullptr;
@@ -294,8 +291,6 @@ struct rt_camera {
         S.off_lights = off_lights;
         S.lds_stack_bytes = 0;
         S.lds_pool_off = 0;
-        S.wpool_k = 0;
-        S.wslots = nullptr;
         S.troot = RT_BVH4 ? build.t4root : build.troot;
         S.root_box = build.troot_box;
         S.cam = build.cam;
@@ -369,7 +364,9 @@ struct rt_camera {
         const bool chunked = env_flag("RT_AMD_CHUNKED", true);
         // Adaptive sampling runs in rounds on the chunked / pool kernels (pt_adapt_kernel
         // settles each round in sample order); RT_AMD_ADAPT_ROUNDS=0 keeps the sequential kernel.
-        const bool rounds = C.adaptive && env_flag("RT_AMD_ADAPT_ROUNDS", true);
+        // Instrumented launches (count == 1) keep the sequential kernel: a round renders samples
+        // past a pixel's convergence, and the work counters would count them.
+        const bool rounds = C.adaptive && count != 1 && env_flag("RT_AMD_ADAPT_ROUNDS", true);
         if (C.n_samples <= 0 || !chunked || (C.adaptive && !rounds)) {
             // sequential-pixel kernel (pixelConverged needs each pixel's samples in one place)
             hip_check(hipEventRecord(pass_event(0, 0), stream), "hipEventRecord");
@@ -395,31 +392,6 @@ struct rt_camera {
                  build.prims.size() < (1u << 14) &&
                  (size_t)S.lds_pool_off + pool_lds_bytes() + static_lds_bytes(count, true) <= (size_t)lds_max &&
                  env_flag("RT_AMD_POOL_KERNEL", true);
-        // Walker-pool kernel (pt_wpool_kernel) for BVH scenes: 64 walkers per wave over K path
-        // slots in HBM. LDS: the walkers' stacks (stride kBlockWPool), the walk data
-        // ([tnodes][tprims][tsph], level 3) when it fits, then the waves' u8 queues. RT_AMD_WPOOL=0/1.
-        int wpool_k = 0;
-        LaunchGeom gw = g;
-        if (!v.emit && (count == 0 || (count == 2 && prec == PREC_REF)) && trav_fast(v.trav) && C.width < 65536 && C.height < 65536 &&
-            C.n_samples <= 65535 && C.depth <= 250 && build.prims.size() < (1u << 20) &&
-            env_flag("RT_AMD_WPOOL", false)) {
-            const int k = std::max(2 * kWave, std::min(env_int("RT_AMD_WPOOL_K", 128), kWPoolMaxK));
-            const size_t wstack = (size_t)std::max(C.stack_depth, 1) * kBlockWPool * sizeof(int);
-            const size_t walk_bytes = (size_t)off_prims;  // [tnodes][tprims][tsph]: the blob's head
-            const size_t stat = static_lds_bytes(count, true);
-            const size_t queues = (size_t)(kBlockWPool / kWave) * wpool_wave_bytes(k);
-            const size_t cap = std::min<size_t>(lds_max, kLdsSceneMaxBytes);
-            gw.lds_level = lds_scene_enabled() && wstack + walk_bytes + queues + stat + 16 <= cap ? 3 : 0;
-            const size_t off = (wstack + (gw.lds_level == 3 ? walk_bytes : 0) + 15) / 16 * 16;
-            if (off + queues + stat <= (size_t)lds_max) {
-                wpool_k = k;
-                S.wpool_k = k;
-                S.lds_pool_off = (int32_t)off;
-                gw.lds_bytes = off + queues;
-                ensure_wslots((size_t)cus * (kBlockWPool / kWave) * (size_t)k * kWPoolSlotBytes);
-                S.wslots = d_wslots;
-            }
-        }
         // guided schedule of `nsamp` samples over `slots` pixel slots: half of the remaining
         // samples per phase, chunks halving. First-phase chunk from the samples per resident
         // lane: an item is the critical path of its pixel, so small per-launch workloads (a
@@ -428,7 +400,6 @@ struct rt_camera {
         // hand-out over long items (tools/tail_probe.py sweep).
         auto schedule = [&](double slots, int nsamp) {
             v.pool = pool_ok;
-            v.wpool = wpool_k > 0;
             // spl: samples per resident lane of this launch.
             const double spl = slots * (double)nsamp / ((double)cus * kBlockChunk);
             // Brute-force scenes in the chunked kernel: two tile-chunks per atomic from 512 spl
@@ -449,11 +420,11 @@ struct rt_camera {
             // (pool kernel, re-tuned at 152 slots per wave: 8 tile-chunks per atomic from 512 spl,
             // 4 from 48, 2 from 24, first items of at most 4 samples - Cornell N=1 14.61 -> 14.43 ms,
             // 1/2 share 7.57 -> 7.40, 1/8 share 2.57 -> 2.10 ms; profiles/r02/sched/)
-            const int pool_auto = (v.pool || v.wpool) ? (spl >= 512.0 ? 8 : spl >= 48.0 ? 4 : spl >= 24.0 ? 2 : 1)
+            const int pool_auto = v.pool ? (spl >= 512.0 ? 8 : spl >= 48.0 ? 4 : spl >= 24.0 ? 2 : 1)
                                  : bvh ? (spl >= 256.0 ? 4 : 2)
                                        : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
-            const int c_max = (v.pool || v.wpool) ? 4 : (bvh && g.lds_level == 0) ? 4 : 32;
+            const int c_max = v.pool ? 4 : (bvh && g.lds_level == 0) ? 4 : 32;
             // (pool kernel, fixed spp, re-checked at the round-3 build: first items of spl / 64, so 4
             // samples for the whole frame and a 1/2 share, 2 for a 1/4 share, 1 for a 1/8 share -
             // Cornell 1/8 share 2.248 -> 2.051 ms, 1/4 3.998 -> 3.931 ms, N=1 and 1/2 unchanged;
@@ -489,7 +460,7 @@ struct rt_camera {
             // the pool kernel keeps log2(item chunk) in a 3-bit slot field (pool_meta): chunks
             // of more than kPoolMaxChunk samples (RT_AMD_CHUNK overrides) take the chunked kernel
             for (int p = 0; p < np; ++p)
-                if (sb.chunk[p] > kPoolMaxChunk) v.pool = v.wpool = false;
+                if (sb.chunk[p] > kPoolMaxChunk) v.pool = false;
             int covered = 0;
             for (int p = 0; p < np; ++p) {
                 if (sb.s0[p] != covered) throw std::runtime_error("guided schedule: gap");
@@ -498,7 +469,7 @@ struct rt_camera {
             if (covered != nsamp) throw std::runtime_error("guided schedule: coverage");
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
-            sb.min_ready = std::min(env_int(v.wpool ? "RT_AMD_WREADY" : "RT_AMD_READY", v.wpool ? 16 : 48), kWave);
+            sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
         };
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;
@@ -515,108 +486,16 @@ struct rt_camera {
             if (items >= (1l << 31) - (1l << 22)) throw std::runtime_error("chunked pass too large");  // counter headroom: 2 x grid waves x pool
             sb.n_items = (int32_t)items;
             if (!first) hip_check(hipMemsetAsync(d_tile, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");
-            LaunchGeom gp = v.wpool ? gw : g;
-            const int block = v.wpool ? kBlockWPool : v.pool ? kBlockPool : kBlockChunk;
+            LaunchGeom gp = g;
+            const int block = v.pool ? kBlockPool : kBlockChunk;
             gp.grid = (int)std::max<long>(1, std::min<long>(items / block + 1, (long)cus));
             DevScene Sp = S;
             if (v.pool) gp.lds_bytes = (size_t)S.lds_pool_off + pool_lds_bytes();
-            if (v.wpool) {
-                Sp.lds_stack_bytes = (int32_t)((size_t)std::max(C.stack_depth, 1) * kBlockWPool * sizeof(int));
-                Sp.lds_words = gw.lds_level == 3 ? off_prims / 16 : 0;
-            }
             // per-pass events: path kernel [0, 1), accumulate [1, 2)
             hip_check(hipEventRecord(pass_event(pass, 0), stream), "hipEventRecord");
             hipError_t e = prec == PREC_FP32 ? launch_render_fp32(v, Sp, reg, out, gp, &sb, stream)
                                              : launch_render_ref(v, Sp, reg, out, gp, &sb, stream);
             hip_check(e, "pt_chunk_kernel launch");
-            hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
-        };
-        // Wavefront passes (wf_shade_kernel / wf_trace_kernel), opt-in (RT_AMD_WAVEFRONT=1) for
-        // fixed-spp ref-precision fast-traversal launches: bit-identical, but on spheres-100k 2048^2
-        // spp16 92 ms against the chunked kernel's 40 ms - the walk-only kernel runs the same
-        // instructions per ray on more lanes (0.45 vs 0.36) yet each of the ~160 iterations ends on
-        // a device-wide drain of its walks, and the path state streams through HBM twice per
-        // iteration (profiles/r03/wavefront/).
-        const bool wf = !rounds && prec == PREC_REF && !v.emit && count == 0 && trav_fast(v.trav) &&
-                        env_int0("RT_AMD_WAVEFRONT", 0) == 1;
-        auto run_pass_wf = [&](bool first) {
-            // the guided schedule over P slots: first items of pow2floor(spl / 4) <= 8 samples
-            // (spl: samples per slot), takes of 4 tile-chunks
-            const long pass_samples = (long)sb.slots * C.n_samples;
-            const long P = std::max<long>(256, std::min<long>((long)env_int("RT_AMD_WF_SLOTS", 8 << 20),
-                                                              (pass_samples / 8 + 255) / 256 * 256));
-            const double spl = (double)pass_samples / (double)P;
-            int c = 1;
-            while (c * 2 <= std::min(8.0, spl / 4.0)) c *= 2;
-            c = std::min(c, std::max(1, C.n_samples / 2));
-            int s0 = 0, np = 0;
-            while (s0 < C.n_samples) {
-                const int rem = C.n_samples - s0;
-                if (c <= 1 || np == kMaxPhases - 1) {
-                    sb.s0[np] = s0; sb.chunk[np] = 1; sb.nch[np] = rem; ++np;
-                    break;
-                }
-                const int span = (rem / 2) / c * c;
-                if (span == 0) { c /= 2; continue; }
-                sb.s0[np] = s0; sb.chunk[np] = c; sb.nch[np] = span / c; ++np;
-                s0 += span;
-                c /= 2;
-            }
-            sb.n_phases = np;
-            for (int q = 0; q < np; ++q) sb.rnch[q] = 1.0 / (double)sb.nch[q];
-            sb.pool = kWave * std::max(1, env_int("RT_AMD_WF_POOL", 4));
-            sb.refill_min = std::min(env_int("RT_AMD_WF_REFILL", 4), kWave);
-            sb.min_ready = std::min(env_int("RT_AMD_WF_READY", 8), kWave);
-            const long group_slots = ((long)sb.slots + kWave - 1) / kWave * kWave;
-            long items = 0;
-            for (int q = 0; q < np; ++q) {
-                sb.item_base[q] = (int32_t)items;
-                items += group_slots * sb.nch[q];
-            }
-            if (items >= (1l << 31) - (1l << 24)) throw std::runtime_error("wavefront pass too large");
-            sb.n_items = (int32_t)items;
-            if (!first) hip_check(hipMemsetAsync(d_tile, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");
-            ensure_wf((size_t)P);
-            WfState W{};
-            W.s0 = d_wf_s[0];
-            W.s1 = d_wf_s[1];
-            W.s2 = d_wf_s[2];
-            W.s3 = reinterpret_cast<int4*>(d_wf_s[3]);
-            W.hit = d_wf_s[4];
-            W.flag = d_wf_flag;
-            W.wpool = d_wf_pool;
-            W.traced = d_wf_traced;
-            W.live = d_wf_live;
-            W.n = (int32_t)P;
-            // one resident wave per SIMD per block: as many blocks per CU as the VGPR bound
-            // (kWfWavesPerSimd) and the walkers' LDS stacks allow - every block resident at once,
-            // since each owns a fixed run of slots (a second round of blocks doubled the time)
-            const size_t trace_lds = (size_t)std::max(C.stack_depth, 1) * kBlockWf * sizeof(int);
-            const int per_cu = std::max(1, std::min<int>(kWfWavesPerSimd, (int)((size_t)lds_max / (trace_lds + 1024))));
-            const int trace_grid = std::max(1, cus * per_cu);
-            const long trace_waves = (long)trace_grid * (kBlockWf / kWave);
-            W.per_wave = (int32_t)(((P + trace_waves - 1) / trace_waves + 255) / 256 * 256);  // whole flag words
-            if (env_flag("RT_AMD_LAUNCH_LOG", false))
-                std::fprintf(stderr, "[rt wavefront] slots %ld stack_depth %d trace blocks/CU %d grid %d slots/wave %d\n",
-                             P, C.stack_depth, per_cu, trace_grid, W.per_wave);
-            hip_check(hipEventRecord(pass_event(pass, 0), stream), "hipEventRecord");
-            hip_check(hipMemsetAsync(d_wf_traced, 0, kWfMaxIter * sizeof(unsigned int), stream), "hipMemsetAsync");
-            hip_check(launch_wf_init(W, sb, stream), "wf_init_kernel launch");
-            constexpr int kBatch = 32;
-            for (int it = 0;; it += kBatch) {
-                if (it + kBatch > kWfMaxIter) throw std::runtime_error("wavefront pass: too many iterations");
-                for (int k = it; k < it + kBatch; ++k)
-                    hip_check(launch_wf_iteration(v.defer, S, reg, out, g.tiles_x, sb, W, k, trace_grid, trace_lds,
-                                                  stream),
-                              "wf_shade / wf_trace launch");
-                hip_check(hipMemcpyAsync(h_wf_traced, d_wf_traced + it, kBatch * sizeof(unsigned int),
-                                         hipMemcpyDeviceToHost, stream),
-                          "hipMemcpyAsync");
-                hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-                bool done = false;
-                for (int k = 0; k < kBatch; ++k) done = done || h_wf_traced[k] == 0u;
-                if (done) break;
-            }
             hip_check(hipEventRecord(pass_event(pass, 1), stream), "hipEventRecord");
         };
         if (rounds) {
@@ -640,15 +519,14 @@ struct rt_camera {
                     sb.stride_s = sb.slots;
                     sb.stride_slot = 1;
                 }
-                if (wf) run_pass_wf(t0 == 0);
-                else run_pass(t0 == 0);
+                run_pass(t0 == 0);
                 hip_check(launch_accum(S, reg, out, g.tiles_x, sb, stream), "pt_accum_kernel launch");
                 hip_check(hipEventRecord(pass_event(pass, 2), stream), "hipEventRecord");
             }
         }
         n_passes = pass;
         ev_accum = true;
-        last_kernel = wf ? RT_KERNEL_WAVEFRONT : v.wpool ? RT_KERNEL_WPOOL : v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
+        last_kernel = v.pool ? RT_KERNEL_POOL : RT_KERNEL_CHUNKED;
     }
 
     // Adaptive sampling in rounds (src/camera.ts:400-425). Round r renders samples
@@ -699,6 +577,7 @@ struct rt_camera {
             ar.len = len;
             ar.next_act = d_act[1 - cur];
             sb.s_base = s_base;
+            sb.err_in_rec = 1;
             schedule((double)n_act, len);
             const size_t rec_per_slot = (size_t)len * sizeof(float4);
             const long pass_slots = std::max<long>(kWave, std::min<long>((n_act + kWave - 1) / kWave * kWave,
@@ -755,53 +634,6 @@ struct rt_camera {
     // Per-sample record buffer of the chunked kernel (grown on demand, kept).
     float4* d_sbuf = nullptr;
     size_t sbuf_cap = 0;
-    // wavefront passes: the slots' state (s0, s1, s2, s3, hit: P float4 each), ray flags, the
-    // shade waves' item ranges and the per-iteration "traced" words (+ a pinned host copy)
-    static constexpr int kWfMaxIter = 1 << 20;
-    float4* d_wf_s[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    uint8_t* d_wf_flag = nullptr;
-    int2* d_wf_pool = nullptr;
-    unsigned long long* d_wf_live = nullptr;
-    unsigned int* d_wf_traced = nullptr;
-    unsigned int* h_wf_traced = nullptr;
-    size_t wf_cap = 0;
-    void free_wf() {
-        for (float4*& q : d_wf_s)
-            if (q) (void)hipFree(q), q = nullptr;
-        if (d_wf_flag) (void)hipFree(d_wf_flag);
-        if (d_wf_pool) (void)hipFree(d_wf_pool);
-        if (d_wf_live) (void)hipFree(d_wf_live);
-        if (d_wf_traced) (void)hipFree(d_wf_traced);
-        if (h_wf_traced) (void)hipHostFree(h_wf_traced);
-        d_wf_flag = nullptr;
-        d_wf_pool = nullptr;
-        d_wf_live = nullptr;
-        d_wf_traced = nullptr;
-        h_wf_traced = nullptr;
-        wf_cap = 0;
-    }
-    void ensure_wf(size_t n) {
-        if (n <= wf_cap) return;
-        free_wf();
-        for (float4*& q : d_wf_s) hip_check(hipMalloc(&q, n * sizeof(float4)), "hipMalloc(wavefront slots)");
-        hip_check(hipMalloc(&d_wf_flag, n), "hipMalloc(wavefront flags)");
-        hip_check(hipMalloc(&d_wf_pool, (n / kWave + 1) * sizeof(int2)), "hipMalloc(wavefront pools)");
-        hip_check(hipMalloc(&d_wf_live, (n / kWave + 1) * sizeof(unsigned long long)), "hipMalloc(wavefront masks)");
-        hip_check(hipMalloc(&d_wf_traced, kWfMaxIter * sizeof(unsigned int)), "hipMalloc(wavefront flags)");
-        hip_check(hipHostMalloc(&h_wf_traced, 64 * sizeof(unsigned int), hipHostMallocDefault), "hipHostMalloc");
-        wf_cap = n;
-    }
-    // walker-pool kernel: the path slots of every resident wave (HBM)
-    float4* d_wslots = nullptr;
-    size_t wslots_cap = 0;
-    void ensure_wslots(size_t bytes) {
-        if (bytes <= wslots_cap) return;
-        if (d_wslots) (void)hipFree(d_wslots);
-        d_wslots = nullptr;
-        wslots_cap = 0;
-        hip_check(hipMalloc(&d_wslots, bytes), "hipMalloc(walker-pool slots)");
-        wslots_cap = bytes;
-    }
     void ensure_sbuf(size_t bytes) {
         if (bytes <= sbuf_cap) return;
         if (d_sbuf) (void)hipFree(d_sbuf);
@@ -1025,29 +857,17 @@ int rt_camera_render_png(rt_camera* cam, int32_t bands, rt_render_stats* stats, 
         cam->ensure_frame();
         const RtCamera& C = cam->build.cam;
         const hipStream_t stream = nullptr;
-        // divideIntoRegions (src/raytracer.ts:185-205): ceil(H / count)-row bands
-        const int count = std::max(1, (int)bands);
-        const int rh = (C.height + count - 1) / count;
-        rt_render_stats m{};
-        m.samples_min = m.bounces_min = INFINITY;
-        for (int b = 0; b < count; ++b) {
-            const int y0 = b * rh, hh = std::min(rh, C.height - y0);
-            if (hh <= 0) break;
-            const rt_region r{0, y0, C.width, hh};
-            cam->launch(r, 0, 1, cam->precision, cam->traversal, 0, cam->d_rgb, nullptr, nullptr, nullptr, 0, stream);
-            rt_render_stats s;
-            cam->read_stats(&s, nullptr, stream);
-            // RenderStats.merge (src/render-utils/renderStats.ts:42-64)
-            m.pixels += s.pixels;
-            m.samples_total += s.samples_total;
-            m.samples_min = std::min(m.samples_min, s.samples_min);
-            m.samples_max = std::max(m.samples_max, s.samples_max);
-            m.bounces_total += s.bounces_total;
-            m.bounces_min = std::min(m.bounces_min, s.bounces_min);
-            m.bounces_max = std::max(m.bounces_max, s.bounces_max);
-        }
-        m.samples_avg = m.pixels > 0 ? m.samples_total / m.pixels : 0.0;
-        m.bounces_avg = m.samples_total > 0 ? m.bounces_total / m.samples_total : 0.0;
+        // The reference renders divideIntoRegions' ceil(H / count)-row bands on `count` workers
+        // (src/raytracer.ts:60-90, 185-205) and merges their RenderStats (renderStats.ts:42-64).
+        // Neither the image nor the merged stats depend on the split (the path RNG is keyed by
+        // pixel and sample; merge sums totals and takes minima / maxima), so the device renders
+        // the whole frame in one launch whatever `bands` says - one launch and one stats read
+        // instead of `bands` small ones, each waiting for the GPU.
+        (void)bands;
+        const rt_region r{0, 0, C.width, C.height};
+        cam->launch(r, 0, 1, cam->precision, cam->traversal, 0, cam->d_rgb, nullptr, nullptr, nullptr, 0, stream);
+        rt_render_stats m;
+        cam->read_stats(&m, nullptr, stream);
         if (stats) *stats = m;
         const std::vector<uint8_t> png = rt_png_encode_device(cam->d_rgb, C.width, C.height, stream);
         uint8_t* b = (uint8_t*)std::malloc(png.size());

@@ -221,11 +221,11 @@ class Camera:
         _lib.check(self._lib.rt_camera_pass_count(self._h, C.byref(n)))
         return int(n.value)
 
-    KERNELS = ("none", "sequential", "chunked", "pool", "wpool", "wavefront")
+    KERNELS = ("none", "sequential", "chunked", "pool")
 
     def last_kernel(self) -> str:
         """Path kernel of the last render (rt_camera_last_kernel): 'sequential',
-        'chunked', 'pool', 'wpool' or 'wavefront' ('none' before any)."""
+        'chunked' or 'pool' ('none' before any)."""
         n = C.c_int32()
         _lib.check(self._lib.rt_camera_last_kernel(self._h, C.byref(n)))
         return self.KERNELS[int(n.value)]

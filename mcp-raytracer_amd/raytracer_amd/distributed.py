@@ -176,9 +176,11 @@ def render_frame(camera, frame, rank: int, world: int, stream=None, precision=No
     assemble them in rank 0's `frame` (HxWx3 uint8 device tensor; `radiance`
     optionally HxWx3 float32). Slab buffers may be passed in to avoid
     reallocation (`slab` / `gathered`: slab_pixels(region, world) pixels, the
-    spare tile holding the stats words). Everything is queued on `stream`
-    (default: torch's current stream of the frame's device), the gather included.
-    Returns rank 0's frame (None on the other ranks when world > 1); with
+    spare tile holding the stats words). The render is queued on `stream`
+    (default: torch's current stream of the frame's device); the gather and the
+    unpack run on torch's current stream (collectives are issued there), and
+    `stream` is then made to wait for them, so rank 0's frame is complete in
+    order on both streams. Returns rank 0's frame (None on the other ranks when world > 1); with
     `stats`, (frame, merged RenderStats) on rank 0 - that waits for the stream."""
     import torch
 
@@ -217,6 +219,7 @@ def render_frame(camera, frame, rank: int, world: int, stream=None, precision=No
     unpack_tiles(g, region, W, H, frame, cur, slab_tiles=n_tiles + 1)
     if radiance is not None:
         unpack_tiles(gr, region, W, H, radiance, cur)
+    _wait_for_current(stream, frame.device)
     if not stats:
         return frame
     w = gathered_stats(g, n_px)
@@ -235,6 +238,19 @@ def _wait(stream, device):
     ev = torch.cuda.Event()
     ev.record(ext)
     cur.wait_event(ev)
+
+
+def _wait_for_current(stream, device):
+    """Make `stream` (a raw hipStream_t) wait for the work queued so far on
+    torch's current stream (the gather and unpack)."""
+    import torch
+
+    cur = torch.cuda.current_stream(device)
+    if stream == cur.cuda_stream:
+        return
+    ev = torch.cuda.Event()
+    ev.record(cur)
+    torch.cuda.ExternalStream(stream, device=device).wait_event(ev)
 
 
 def _sync(stream):

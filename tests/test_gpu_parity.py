@@ -232,6 +232,24 @@ def test_work_counters_match_oracle(rt, oracle, gpu):
         assert abs(cnt[k] - orc[k]) <= 0.01 * orc[k] + 2, (k, cnt[k], orc[k])
 
 
+def test_work_counters_adaptive_count_the_references_samples(rt, oracle, gpu):
+    """with adaptive sampling on, an instrumented launch runs the sequential kernel
+    (adaptive rounds would render - and count - samples past each pixel's convergence), so the
+    counters are the work of exactly the reference's samples."""
+    import torch
+    sd = rt.generate_scene_data({"type": "cornell"})
+    ro = {"width": 32, "samples": 60, "depth": 16, "aTolerance": 0.05, "aBatch": 10}
+    cam = rt.create_camera_from_scene_data(sd, {**ro, "traversal": "reference"})
+    buf = torch.zeros((32, 32, 3), dtype=torch.uint8, device="cuda")
+    st, cnt = cam.render_device(rgb_ptr=buf.data_ptr(), synchronize=True, count_work=True)
+    assert cam.last_kernel() == "sequential"
+    orc = oracle.render(sd, ro, counters=True)
+    assert st.samples["total"] == orc["stats"]["samples"]["total"] < 32 * 32 * 60  # some pixels converged
+    assert cnt["samples"] == orc["counters"]["samples"]
+    for k in ["rays", "node", "sphere", "quad", "material", "light_quad", "bounces", "diffuse"]:
+        assert abs(cnt[k] - orc["counters"][k]) <= 0.01 * orc["counters"][k] + 2, (k, cnt[k], orc["counters"][k])
+
+
 def test_world_hit_matches_oracle(rt, oracle, gpu):
     rng = np.random.default_rng(7)
     for cfg in [{"type": "spheres", "options": {"count": 200, "seed": 3}}, {"type": "cornell"}, {"type": "default"}]:
@@ -284,6 +302,63 @@ def test_missing_background_raises_like_reference(rt, gpu):
     sd2["camera"]["vfov"] = 10
     cam2 = rt.create_camera_from_scene_data(sd2, {"width": 8, "samples": 1, "depth": 1, **NOADAPT})
     cam2.render(np.zeros((8, 8, 3), np.uint8))
+
+
+def _slit_box(gap):
+    """A closed box [-1, 1]^3 around the camera with an emissive ceiling and a slit of width
+    `gap` along one edge of the wall behind the camera, no background: a path misses (and
+    the reference throws "reading 'top'") only when it leaves through the slit."""
+    return {
+        "camera": {"vfov": 60, "from": [0, 0, 0.5], "at": [0, 0, -1], "up": [0, 1, 0], "aperture": 0.0, "focus": 0},
+        "render": {"aspect": 1},
+        "materials": [
+            {"id": "white", "material": {"type": "lambert", "color": [0.73, 0.73, 0.73]}},
+            {"id": "red", "material": {"type": "lambert", "color": [0.65, 0.05, 0.05]}},
+            {"id": "lamp", "material": {"type": "light", "emit": [1, 1, 1]}},
+        ],
+        "objects": [
+            {"type": "quad", "pos": [-1, -1, -1], "u": [2, 0, 0], "v": [0, 2, 0], "material": "white"},
+            {"type": "quad", "pos": [-1, -1, 1], "u": [2 - gap, 0, 0], "v": [0, 2, 0], "material": "white"},
+            {"type": "quad", "pos": [-1, -1, -1], "u": [0, 0, 2], "v": [0, 2, 0], "material": "red"},
+            {"type": "quad", "pos": [1, -1, -1], "u": [0, 0, 2], "v": [0, 2, 0], "material": "white"},
+            {"type": "quad", "pos": [-1, -1, -1], "u": [2, 0, 0], "v": [0, 0, 2], "material": "white"},
+            {"type": "quad", "pos": [-1, 1, -1], "u": [2, 0, 0], "v": [0, 0, 2], "material": "lamp", "light": True},
+        ],
+    }
+
+
+@pytest.mark.parametrize("path", ["pool", "chunked", "fast"])
+def test_adaptive_rounds_ignore_misses_past_convergence(rt, oracle, gpu, path, monkeypatch):
+    """adaptive rounds render samples past a pixel's convergence, which the
+    reference's loop never renders (src/camera.ts:400-425). A miss among THOSE samples must
+    not raise. Premise, checked with the oracle: pixel (0, 0) of the slit box (seed 1,
+    aTolerance 0.3) converges after 60 samples without a miss, while its samples 0..199 do
+    miss (first at index 71) - and a one-pixel region's second round renders samples [10, 200)
+    (after a round retiring < 10 % of the pixels the next one takes every remaining sample)."""
+    sd = _slit_box(0.05)
+    ro = {"width": 16, "samples": 200, "depth": 16, "aTolerance": 0.3, "aBatch": 10, "seed": 1}
+    if path == "fast":
+        ro["traversal"] = "fast"
+    if path == "chunked":
+        monkeypatch.setenv("RT_AMD_POOL_KERNEL", "0")
+    region = (0, 0, 1, 1)
+    orc = oracle.render(sd, ro, region=region)
+    assert int(orc["px_samples"][0, 0]) == 60
+    with pytest.raises(Exception, match="reading 'top'"):
+        oracle.render(sd, {**ro, "aTolerance": 0}, region=region)
+    oracle.render(sd, {**ro, "aTolerance": 0, "samples": 71}, region=region)  # samples 0..70 hit
+    with pytest.raises(Exception, match="reading 'top'"):
+        oracle.render(sd, {**ro, "aTolerance": 0, "samples": 72}, region=region)
+    cam, rgb, rad, st = _render_gpu(rt, sd, ro, region=region)
+    assert cam.last_kernel() == ("chunked" if path != "pool" else "pool")
+    rounds, rendered = cam.adaptive_info()
+    assert rounds == 2 and rendered >= 200  # the second round rendered sample 71
+    assert_identical(rad[:1, :1], rgb[:1, :1], orc["radiance"][:1, :1], orc["rgb"][:1, :1], f"slit box {path}")
+    assert_stats_identical(st, orc["stats"])
+    # fixed spp renders sample 71 for real: the reference's error
+    cam2 = rt.create_camera_from_scene_data(sd, {**ro, "aTolerance": 0})
+    with pytest.raises(rt.RtError, match="reading 'top'"):
+        cam2.render_region(np.zeros((16, 16, 3), np.uint8), region)
 
 
 def test_generate_image_buffer_png(rt, gpu):
@@ -975,189 +1050,6 @@ def test_adaptive_full_size_headline_rows_match_oracle(rt, oracle, gpu):
         del os.environ["RT_AMD_ADAPT_ROUNDS"]
     assert_identical(rad, rgb, rad2, rgb2, "adaptive 800 rounds == sequential")
     assert st.samples == st2.samples and st.bounces == st2.bounces
-
-
-# ---------------------------------------------------------------------------
-# Walker-pool kernel (pt_wpool_kernel, BVH scenes): 64 walkers per wave over LDS
-# path slots with trace / shade / start queues. Same records as the chunked
-# kernel, so images and stats are bit-identical to it and to the oracle.
-# ---------------------------------------------------------------------------
-WPOOL_CASES = {
-    "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
-                {"width": 48, "aspect": 1, "samples": 8, "depth": 8, **NOADAPT}),
-    "rain": ({"type": "rain", "options": {"seed": 42}}, {"width": 64, "samples": 8, "depth": 16, **NOADAPT}),
-    "spheres_deep": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
-                     {"width": 40, "aspect": 1, "samples": 6, "depth": 120, **NOADAPT}),
-    "spheres_adaptive": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
-                         {"width": 48, "aspect": 1, "samples": 40, "depth": 8, "aTolerance": 0.1}),
-    "spheres_aperture": ({"type": "spheres", "options": {"count": 200, "seed": 7}},
-                         {"width": 40, "aspect": 1.5, "samples": 5, "depth": 10, **NOADAPT}),
-}
-
-
-@pytest.mark.parametrize("case", sorted(WPOOL_CASES))
-def test_wpool_kernel_matches_oracle_and_chunked(rt, oracle, gpu, case, monkeypatch):
-    cfg, ro = WPOOL_CASES[case]
-    sd = rt.generate_scene_data(cfg)
-    if case == "spheres_aperture":
-        sd["camera"]["aperture"] = 0.1
-    monkeypatch.setenv("RT_AMD_WPOOL", "1")
-    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
-    assert cam.last_kernel() == "wpool"
-    orc = oracle.render(sd, ro)
-    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wpool {case}")
-    assert_stats_identical(st, orc["stats"])
-    monkeypatch.setenv("RT_AMD_WPOOL", "0")
-    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
-    assert cam2.last_kernel() == "chunked"
-    assert_identical(rad, rgb, rad2, rgb2, f"wpool == chunked {case}")
-
-
-@pytest.mark.parametrize("seed", range(6))
-def test_wpool_random_scenes_match_oracle(rt, oracle, gpu, seed, monkeypatch):
-    sd = _random_scene(seed)
-    ro = {"width": 32, "samples": 4, "depth": 8, **NOADAPT, "traversal": "fast"}
-    orc = oracle.render(sd, ro)
-    monkeypatch.setenv("RT_AMD_WPOOL", "1")
-    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
-    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wpool random {seed} ({cam.last_kernel()})")
-    assert_stats_identical(st, orc["stats"])
-
-
-def test_wpool_small_pool_and_tiny_slot_counts(rt, oracle, gpu, monkeypatch):
-    """The smallest admissible pool (2 x 64 slots) and a launch with fewer pixels
-    than walkers (a 3x5 region), regions and tile groups."""
-    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 500, "seed": 42}})
-    ro = {"width": 40, "aspect": 1, "samples": 7, "depth": 8, **NOADAPT}
-    orc = oracle.render(sd, ro)
-    monkeypatch.setenv("RT_AMD_WPOOL", "1")
-    monkeypatch.setenv("RT_AMD_WPOOL_K", "128")
-    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
-    assert cam.last_kernel() == "wpool"
-    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], "wpool K=128")
-    monkeypatch.delenv("RT_AMD_WPOOL_K")
-    cam = rt.create_camera_from_scene_data(sd, ro)
-    rgb2 = np.zeros_like(rgb)
-    rad2 = np.zeros_like(rad)
-    cam.render_region(rgb2, (17, 11, 3, 5), radiance=rad2)
-    assert cam.last_kernel() == "wpool"
-    assert_identical(rad2[11:16, 17:20], rgb2[11:16, 17:20], orc["radiance"][11:16, 17:20], orc["rgb"][11:16, 17:20],
-                     "wpool 3x5 region")
-    assert not rgb2[:11].any() and not rgb2[16:].any()
-
-
-def test_wpool_full_size_spheres500_rows_match_oracle(rt, oracle, gpu, monkeypatch):
-    """BASELINE config 2 (spheres-500, 800x800, spp 64, depth 8) through the
-    walker pool: whole frame equal to the chunked kernel's, oracle rows exact."""
-    cfg, ro, rows = FULL["spheres"]
-    ro = {**ro, **NOADAPT}
-    sd = rt.generate_scene_data(cfg)
-    monkeypatch.setenv("RT_AMD_WPOOL", "1")
-    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
-    assert cam.last_kernel() == "wpool"
-    W, H = cam.image_width, cam.image_height
-    for y in rows:
-        orc = oracle.render(sd, ro, region=(0, y, W, 1), threads=8)
-        assert_identical(rad[y:y + 1], rgb[y:y + 1], orc["radiance"][y:y + 1], orc["rgb"][y:y + 1],
-                         f"wpool spheres-500 row {y}")
-    monkeypatch.setenv("RT_AMD_WPOOL", "0")
-    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
-    assert_identical(rad, rgb, rad2, rgb2, "wpool == chunked spheres-500 800^2")
-    assert st.bounces == st2.bounces
-
-
-# ---------------------------------------------------------------------------
-# Wavefront passes (wf_shade_kernel / wf_trace_kernel; automatic for large launches of
-# trees walked from global memory, forced here with RT_AMD_WAVEFRONT=1 on small ones).
-# Same records as the chunked kernel: images and stats bit-identical to it and the oracle.
-# ---------------------------------------------------------------------------
-WF_CASES = {
-    "spheres": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
-                {"width": 48, "aspect": 1, "samples": 8, "depth": 8, **NOADAPT}, {}),
-    "rain": ({"type": "rain", "options": {"seed": 42}}, {"width": 64, "samples": 8, "depth": 16, **NOADAPT}, {}),
-    "spheres_deep": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
-                     {"width": 40, "aspect": 1, "samples": 6, "depth": 120, **NOADAPT}, {}),
-    "spheres_aperture": ({"type": "spheres", "options": {"count": 200, "seed": 7}},
-                         {"width": 40, "aspect": 1.5, "samples": 5, "depth": 10, **NOADAPT}, {}),
-    # few slots: every slot runs many items; several trace waves per slot run
-    "spheres_few_slots": ({"type": "spheres", "options": {"count": 500, "seed": 42}},
-                          {"width": 40, "aspect": 1, "samples": 9, "depth": 8, **NOADAPT}, {"RT_AMD_WF_SLOTS": "256"}),
-    # several record passes (1 MB budget)
-    "spheres_multipass": ({"type": "spheres", "options": {"count": 500, "seed": 42}},  # 96^2 x 16 x 16 B: 3 passes
-                          {"width": 96, "aspect": 1, "samples": 16, "depth": 8, **NOADAPT}, {"RT_AMD_SBUF_MB": "1"}),
-    "spheres2k_deferred": ({"type": "spheres", "options": {"count": 2000, "seed": 5}},
-                           {"width": 40, "aspect": 1, "samples": 6, "depth": 12, **NOADAPT}, {"RT_AMD_DEFER": "1"}),
-}
-
-
-@pytest.mark.parametrize("case", sorted(WF_CASES))
-def test_wavefront_matches_oracle_and_chunked(rt, oracle, gpu, case, monkeypatch):
-    cfg, ro, env = WF_CASES[case]
-    sd = rt.generate_scene_data(cfg)
-    if case == "spheres_aperture":
-        sd["camera"]["aperture"] = 0.1
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
-    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
-    assert cam.last_kernel() == "wavefront"
-    if case == "spheres_multipass":
-        assert cam.pass_count() > 1
-    orc = oracle.render(sd, ro)
-    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wavefront {case}")
-    assert_stats_identical(st, orc["stats"])
-    monkeypatch.setenv("RT_AMD_WAVEFRONT", "0")
-    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
-    assert cam2.last_kernel() == "chunked"
-    assert_identical(rad, rgb, rad2, rgb2, f"wavefront == chunked {case}")
-
-
-@pytest.mark.parametrize("seed", range(4))
-def test_wavefront_random_scenes_match_oracle(rt, oracle, gpu, seed, monkeypatch):
-    sd = _random_scene(seed)
-    ro = {"width": 32, "samples": 4, "depth": 8, **NOADAPT, "traversal": "fast"}
-    orc = oracle.render(sd, ro)
-    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
-    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
-    assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"wavefront random {seed} ({cam.last_kernel()})")
-    assert_stats_identical(st, orc["stats"])
-
-
-def test_wavefront_regions_and_tile_groups(rt, oracle, gpu, monkeypatch):
-    """A region smaller than a tile and an 8-way tile split through the wavefront path."""
-    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 500, "seed": 42}})
-    ro = {"width": 40, "aspect": 1, "samples": 7, "depth": 8, **NOADAPT}
-    orc = oracle.render(sd, ro)
-    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
-    cam = rt.create_camera_from_scene_data(sd, ro)
-    rgb2 = np.zeros_like(orc["rgb"])
-    rad2 = np.zeros_like(orc["radiance"])
-    cam.render_region(rgb2, (17, 11, 3, 5), radiance=rad2)
-    assert cam.last_kernel() == "wavefront"
-    assert_identical(rad2[11:16, 17:20], rgb2[11:16, 17:20], orc["radiance"][11:16, 17:20], orc["rgb"][11:16, 17:20],
-                     "wavefront 3x5 region")
-    assert not rgb2[:11].any() and not rgb2[16:].any()
-    import torch
-    H, W = orc["rgb"].shape[:2]
-    frame = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
-    for g in range(8):
-        cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=g, tile_groups=8, synchronize=True)
-    assert np.array_equal(frame.cpu().numpy(), orc["rgb"])
-
-
-def test_wavefront_spheres100k_2048_rows_match_oracle(rt, oracle, gpu, monkeypatch):
-    """spheres-100k 2048x2048 spp 16 (2^26 samples, tree in global memory) through the
-    wavefront passes: oracle row segments exact."""
-    sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 100000, "seed": 42}})
-    ro = {"width": 2048, "aspect": 1, "samples": 16, "depth": 100, **NOADAPT}
-    monkeypatch.setenv("RT_AMD_WAVEFRONT", "1")
-    cam, rgb, rad, st = _render_gpu(rt, sd, ro)
-    assert cam.last_kernel() == "wavefront"
-    assert st.samples["total"] == 2048 * 2048 * 16
-    for (x, y) in [(1022, 950), (500, 1500), (1500, 300)]:
-        orc = oracle.render(sd, ro, region=(x, y, 16, 1), threads=16)
-        assert_identical(rad[y:y + 1, x:x + 16], rgb[y:y + 1, x:x + 16], orc["radiance"][y:y + 1, x:x + 16],
-                         orc["rgb"][y:y + 1, x:x + 16], f"spheres-100k 2048^2 row {y} x {x}")
 
 
 # ---------------------------------------------------------------------------

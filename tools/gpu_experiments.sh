@@ -1,11 +1,8 @@
 #!/bin/bash
 # Round-3 A/B experiments behind profiles/r03/ (one parameterised script; run from the repo root
 # on the GPU box). usage: TAG=<out> bash tools/gpu_experiments.sh <experiment>
-#   wpool_ab   walker-pool parity tests, then bench arms (RT_AMD_WPOOL / RT_AMD_WPOOL_K) on
-#              spheres-500, rain 1080p spp128, spheres-100k 2048² spp16   -> profiles/r03/wpool_hbm/
-#   wf_ab      wavefront parity tests, then RT_AMD_WAVEFRONT=0/1 arms      -> profiles/r03/wavefront/
-#   wf_prof    rocprofv3 kernel stats: wavefront vs chunked, spheres-100k 2048² spp16
-#   wf_pmc     counter passes (VALU, lanes, waits, L2 hit): wavefront vs chunked
+#   (wpool_ab / wf_ab / wf_prof / wf_pmc: the round-3 walker-pool and wavefront arms, retired with those
+#    kernels in round 4 - DESIGN.md §4; their logs stay under profiles/r03/)
 #   tail_ab    rank-0 shares N = 1..8 (tools/rank_share.py) under $ARMS env settings -> profiles/r03/tail/
 #   variant_ab parity tests (-k $KSEL) on the variant libraries in $VARIANTS, then bench arms
 #              (Cornell ref / fp32 unless $CFGS) for the product library and each variant
@@ -29,40 +26,6 @@ ab() {  # ab <pytest -k expr> <default CFGS> <default ARMS>
   python tools/ab_table.py $OUT > $OUT/table.txt
 }
 case $1 in
-  wpool_ab)
-    ab wpool "spheres --scene spheres --spp 64 --depth 8
-rain --scene rain --width 1920 --spp 128 --depth 16
-s100k $S100K" "base RT_AMD_WPOOL=0
-wp RT_AMD_WPOOL=1
-wpk192 RT_AMD_WPOOL=1 RT_AMD_WPOOL_K=192
-wpk255 RT_AMD_WPOOL=1 RT_AMD_WPOOL_K=255" ;;
-  wf_ab)
-    ab wavefront "s100k $S100K
-spheres --scene spheres --spp 64 --depth 8" "chunked RT_AMD_WAVEFRONT=0
-wf RT_AMD_WAVEFRONT=1" ;;
-  wf_prof)
-    A="$S100K --no-cpu --no-count --no-parity --steps 2 --warmup 1"
-    cd /tmp && export TMPDIR=/tmp
-    for arm in 1 0; do
-      RT_AMD_WAVEFRONT=$arm timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/wf$arm -o run --output-format csv \
-        -- python3 $R/bench.py $A > $R/$O/wf$arm.log 2>&1 || exit $?
-    done ;;
-  wf_pmc)
-    A="$S100K --no-cpu --no-count --no-parity --steps 1 --warmup 0"
-    cd /tmp && export TMPDIR=/tmp
-    i=0
-    while read -r line; do
-      i=$((i+1))
-      for arm in 1 0; do
-        RT_AMD_WAVEFRONT=$arm timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $line -d $R/$O/wf${arm}_p$i -o run \
-          --output-format csv -- python3 $R/bench.py $A > $R/$O/wf${arm}_p$i.log 2>&1 || exit $?
-      done
-    done <<'PASSES'
-SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE
-SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES
-TCC_HIT_sum TCC_MISS_sum
-PASSES
-    ;;
   tail_ab)
     echo "${ARMS:-base RT_AMD_TAIL=0}" | while read -r arm envs; do
       [ -z "$arm" ] && continue
