@@ -74,7 +74,12 @@ def algorithmic_bytes(c: dict, pixels: int) -> float:
 
 def cpu_baseline(scene_data, ropts, width, height, spp, target_s=15.0):
     """The CPU restatement (oracle, ref precision, 1 thread) on a bounded row
-    subsample of the same workload."""
+    subsample of the same workload. The oracle restates the reference's object
+    model (virtual Hittable.hit / Material.scatter, a recursive rayColor, a
+    MixturePDF allocated per diffuse bounce, as src/camera.ts:263-315 does): the
+    stand-in for the single-threaded TypeScript path, which cannot run here
+    (SURVEY.md §8c). Beside it: the same restatement over the host cores
+    (`multi_core`) and in fp32 scalars (`fp32`, BASELINE.md §4's row)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
 
@@ -98,7 +103,18 @@ def cpu_baseline(scene_data, ropts, width, height, spp, target_s=15.0):
             else f"{region[2]} px of row {region[1]}")
     line = {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
             "sample": f"{what} at spp={spp} ({int(out['stats']['pixels'])} px, {int(samples)} samples, "
-                      f"{dt:.1f} s), oracle/oracle.cpp ref precision, single thread"}
+                      f"{dt:.1f} s), oracle/oracle.cpp ref precision (the reference's object model: virtual "
+                      f"hit/scatter, per-bounce MixturePDF allocation), single thread"}
+    # the same restatement with fp32 scalars, single thread, about half the work
+    step32 = step * 2
+    t0 = time.perf_counter()
+    out = pyoracle.render(scene_data, ropts, row_step=step32, threads=1, region=region, precision="fp32")
+    dt32 = time.perf_counter() - t0
+    s32 = out["stats"]["samples"]["total"]
+    line["fp32"] = {"value": s32 / dt32 / 1e6, "unit": "Msamples/s", "cores": 1,
+                    "sample": f"rows j%{step32}==0 ({int(s32)} samples, {dt32:.1f} s), oracle/oracle.cpp fp32 "
+                              f"scalars, single thread" if region is None else
+                              f"{region[2]} px of row {region[1]} ({int(s32)} samples, {dt32:.1f} s), fp32 scalars"}
     # the same restatement over all of this process's host cores
     # (threads over rows, the analogue of the reference's -p workers), ~target_s/2 of work.
     # The GPU box grants a 16-CPU share whatever nproc says.

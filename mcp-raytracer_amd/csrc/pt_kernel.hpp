@@ -584,6 +584,7 @@ struct FRay {
     float inv[3];  // 1/d with zero components replaced by +-1e-30 (no 0*inf NaNs)
     float noi[3];  // -(o * inv): the slab planes' t = fma(b, inv, noi)
     float eps;     // absolute t slack of the fused slab test (>= 2u max|o * inv|, see slab_t)
+    float pthr;    // |d[a]| at or below which an axis quad counts as near-parallel (inf: every one)
     float a;       // |d|^2
     float ia;      // ~1/|d|^2
     float on;      // |o| (rounded up)
@@ -606,14 +607,16 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
     }
     // 1e-6 * max|o * inv| ~ 16 u: covers the rounding of o * inv at both ends of the interval
     f.eps = m * 1e-6f;
+    f.a = d.x * d.x + d.y * d.y + d.z * d.z;
+    f.ia = __builtin_amdgcn_rcpf(f.a);
+    f.dn = __builtin_amdgcn_sqrtf(f.a) * (1.0f + kRel);
+    f.pthr = 1e-3f * f.dn;
     if (!(m < 1e37f)) {  // o * inv overflowed (|o| > ~1e7 with an axis-parallel d): cull nothing
 #pragma unroll
         for (int a = 0; a < 3; ++a) f.inv[a] = f.noi[a] = 0.0f;
         f.eps = __builtin_inff();
+        f.pthr = __builtin_inff();  // and every axis quad is decided exactly
     }
-    f.a = d.x * d.x + d.y * d.y + d.z * d.z;
-    f.ia = __builtin_amdgcn_rcpf(f.a);
-    f.dn = __builtin_amdgcn_sqrtf(f.a) * (1.0f + kRel);
     f.on = __builtin_amdgcn_sqrtf(o.x * o.x + o.y * o.y + o.z * o.z) * (1.0f + kRel);
     return f;
 }
@@ -653,15 +656,13 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 // the nearest hit child is returned as the next reference and the other hit children are
 // pushed farthest first (so the nearer pop first); with no hit child the next reference is
 // popped (kTravDone when the stack is empty). Branch-free:
-//  * each child's key is its entry distance's bits (a positive float orders as its bits)
-//    with the low two bits replaced by the child index, or ~0 for a miss / empty slot, so
-//    the four keys sort with a 5-exchange min/max network of u32 (10 VALU, instead of
-//    carrying (distance, reference) pairs through selects); two entry distances within
-//    4 ulps may come out in child order - that only changes the visiting order, which
-//    never changes the (t, slot) minimum the walk returns;
-//  * the references of the sorted keys are re-read from the node (its row of refs, in
-//    LDS or L1);
-//  * with n hit children the keys s1..s3 are written in the order s3, s2, s1 at stack
+//  * each child's key is its entry distance's bits (a positive float orders as its bits), or
+//    ~0 for a miss / empty slot; (key, reference) pairs go through a 5-exchange network
+//    (one compare, min / max of the keys, two selects of the references per exchange).
+//    (Round 4 also tried keys carrying the child index in their low two bits, sorted alone
+//    with min / max and the references re-read from the node afterwards: 4 dependent loads
+//    per step - spheres-100k, whose tree is walked from global memory, lost 14 %.)
+//  * with n hit children the pairs s1..s3 are written in the order s3, s2, s1 at stack
 //    positions sp + max(n - 1 - j, 0), so s_{n-1} .. s1 land at sp .. sp + n - 2 and the
 //    writes of missed children land at sp, overwritten or above the new top. No write
 //    goes past sp + 2: at a node of level L (root 1) the stack holds at most 3 (L - 1)
@@ -681,6 +682,7 @@ __device__ __forceinline__ int t4_step(const RtT4Node* nd0, const FRay& f, float
     const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
     const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
     uint32_t k[4];
+    int r[4];
     int n = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -693,25 +695,24 @@ __device__ __forceinline__ int t4_step(const RtT4Node* nd0, const FRay& f, float
             tf = ::fminf(tf, ::fmaxf(t0, t1));
         }
         const bool hit = (cr[c] != kT4Empty) & slab_accept(tn, tf, f);
-        k[c] = hit ? ((__float_as_uint(tn) & ~3u) | (uint32_t)c) : ~0u;
+        k[c] = hit ? __float_as_uint(tn) : ~0u;
+        r[c] = cr[c];
         n += hit ? 1 : 0;
     }
     auto cx = [&](int i, int j) {
-        const uint32_t lo = min(k[i], k[j]);
-        k[j] = max(k[i], k[j]);
+        const bool sw = k[j] < k[i];
+        const uint32_t lo = min(k[i], k[j]), hi = max(k[i], k[j]);
+        const int ri = r[i], rj = r[j];
         k[i] = lo;
+        k[j] = hi;
+        r[i] = sw ? rj : ri;
+        r[j] = sw ? ri : rj;
     };
     cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-    // every read before the first write (the stack and the node may share LDS: the compiler
-    // would otherwise wait out each read before the following write)
-    const int* refs = nd->ref;
-    int rs[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) rs[j] = refs[k[j] & 3u];
     const int popped = stk[max(sp - 1, 0) * STRIDE];
 #pragma unroll
-    for (int j = 3; j >= 1; --j) stk[max(sp + n - 1 - j, sp) * STRIDE] = rs[j];
-    const int next = n > 0 ? rs[0] : (sp > 0 ? popped : kT4Empty);  // (kT4Empty = kTravDone)
+    for (int j = 3; j >= 1; --j) stk[max(sp + n - 1 - j, sp) * STRIDE] = r[j];
+    const int next = n > 0 ? r[0] : (sp > 0 ? popped : kT4Empty);  // (kT4Empty = kTravDone)
     sp = n > 0 ? sp + n - 1 : max(sp - 1, 0);
     return next;
 }
@@ -1289,31 +1290,33 @@ __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Rea
     return true;
 }
 
-// The brute-force pass's version over an RtPre record {n[a], D, Q[ia], Q[ib], w_a*v, w_a*u,
-// max(|Q[ia]|, |Q[ib]|)}: the hit-point error of both in-plane coordinates bounded by one
-// per-ray term (|o| <= on, |d| <= dn, |Q| <= qm), alpha and beta through the host-folded
-// products - fewer operations, a (slightly) wider but still conservative margin.
+// The brute-force pass's axis-quad pre-filter over an RtPre record {x_a, sv, su, -Q[ia] sv,
+// -Q[ib] su, qm = max(|Q[ia]|, |Q[ib]|)}. The plane's t comes from the ray's slab constants,
+// t = fma(x_a, inv[a], noi[a]), instead of a reciprocal of n.d per quad, and alpha / beta are
+// two FMAs each on host-folded products (round 4: 45 -> ~20 VALU per quad).
+// Error: x_a and noi are rounded (the exact test divides D - n.o by n.d in double), and inv is
+// v_rcp's (<= 1 ulp): |t - t_exact| <= ~4u (|x_a inv| + |noi|) + 2^-23 |t| <= kRel (|t| + |noi|),
+// since |x_a inv| <= |t| + |noi| (u = 2^-24, kRel ~ 168 u). The in-plane coordinate
+// o + t d - Q is off by at most et |d| + a few u (|o| + |t d| + |Q|) <= dp below (|o| <= on,
+// |d| <= dn, |Q| <= qm), times |sv| (|su|) in alpha (beta), plus the 1e-4 absolute that
+// covers alpha's own rounding near [0, 1]. Near-parallel rays (|d[a]| <= 1e-3 |d|, or a ray
+// whose slab constants overflowed: pthr = inf) are decided by the exact test.
 template <int CODE>
 __device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, float& lo) {
     RT_FP32_FUSED
     constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
     constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
-    const float na = v[0], D = v[1], q1 = v[2], q2 = v[3], asv = v[4], asu = v[5], qm = v[6];
-    const float denom = na * f.d[a];
+    const float xa = v[0], sv = v[1], su = v[2], nq1 = v[3], nq2 = v[4], qm = v[5];
     lo = kTminLo;
-    if (!(::fabsf(denom) > 1e-3f * f.dn)) return true;  // near-parallel: decide exactly
-    const float no = na * f.o[a];
-    // (idn = na * f.inv[a], the FRay's 1/d instead of a reciprocal per quad: 14.53 -> 14.74 ms on
-    // Cornell, profiles/r03/exp2/ - measured and dropped)
-    const float idn = __builtin_amdgcn_rcpf(denom);
-    const float t = (D - no) * idn;
-    const float et = kRel * ((::fabsf(D) + ::fabsf(no)) * ::fabsf(idn) + 2.0f * ::fabsf(t)) + 1e-30f;
+    if (!(::fabsf(f.d[a]) > f.pthr)) return true;
+    const float t = __builtin_fmaf(xa, f.inv[a], f.noi[a]);
+    const float et = kRel * (::fabsf(t) + ::fabsf(f.noi[a])) + 1e-30f;
     if (t + et < kTminLo) return false;
     lo = t - et;
-    const float alpha = (f.o[ia] + t * f.d[ia] - q1) * asv;
-    const float beta = (f.o[ib] + t * f.d[ib] - q2) * asu;
+    const float alpha = __builtin_fmaf(__builtin_fmaf(t, f.d[ia], f.o[ia]), sv, nq1);
+    const float beta = __builtin_fmaf(__builtin_fmaf(t, f.d[ib], f.o[ib]), su, nq2);
     const float dp = et * f.dn + kRel * (f.on + ::fabsf(t) * f.dn + qm);
-    const float ea = ::fabsf(asv) * dp + 1e-4f, eb = ::fabsf(asu) * dp + 1e-4f;
+    const float ea = ::fabsf(sv) * dp + 1e-4f, eb = ::fabsf(su) * dp + 1e-4f;
     return !(alpha < -ea || alpha > 1.0f + ea || beta < -eb || beta > 1.0f + eb);
 }
 

@@ -186,13 +186,15 @@ struct rt_camera {
                 const int a = (code - 1) % 3, vflag = (code - 1) / 3;
                 const int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
                 q.kind = code;
-                q.f[0] = p.g3[a];
-                q.f[1] = p.g0[3];
-                q.f[2] = p.g0[ia];
-                q.f[3] = p.g0[ib];
-                q.f[4] = p.g3[3] * p.g2[3];  // w_a * v (alpha's factor)
-                q.f[5] = p.g3[3] * p.g1[3];  // w_a * u (beta's factor)
-                q.f[6] = std::max(std::fabs(p.g0[ia]), std::fabs(p.g0[ib]));
+                const double asv = (double)p.g3[3] * (double)p.g2[3];  // w_a * v (alpha's factor)
+                const double asu = (double)p.g3[3] * (double)p.g1[3];  // w_a * u (beta's factor)
+                q.f[0] = (float)(p.s0 / (double)p.g3[a]);          // the plane x_a = D / n_a
+                q.f[1] = (float)asv;
+                q.f[2] = (float)asu;
+                q.f[3] = (float)(-(double)p.g0[ia] * asv);
+                q.f[4] = (float)(-(double)p.g0[ib] * asu);
+                q.f[5] = std::max(std::fabs(p.g0[ia]), std::fabs(p.g0[ib]));
+                q.f[6] = 0.0f;
             } else {
                 q.kind = PRE_OTHER;
             }

@@ -98,9 +98,9 @@ static_assert(sizeof(RtMat) == 64, "RtMat must be 64 bytes");
 // Compact brute-force pre-filter record per primitive (slot order): everything the
 // fp32 pre-filter of a sphere or an axis-aligned quad reads, in one 32-byte scalar
 // load (the full RtPrim takes two dependent loads for a quad: its type, then its
-// axis code). kind: PRE_SPHERE {cx, cy, cz, r}; 1..6 = axis code {n[a], D, Q[ia],
-// Q[ib], +-w[a]*v[iv], +-w[a]*u[iu], max(|Q[ia]|, |Q[ib]|)} (scene.cpp encode_axis_quad);
-// PRE_OTHER: read the RtPrim.
+// axis code). kind: PRE_SPHERE {cx, cy, cz, r}; 1..6 = axis code {x_a of the plane (D / n[a]),
+// sv = +-w[a]*v[iv], su = +-w[a]*u[iu], -Q[ia]*sv, -Q[ib]*su, max(|Q[ia]|, |Q[ib]|), 0}
+// (scene.cpp encode_axis_quad, rt_api.cpp prefilter_records); PRE_OTHER: read the RtPrim.
 enum : int32_t { PRE_SPHERE = 0, PRE_OTHER = 7 };
 struct alignas(16) RtPre {
     int32_t kind;

@@ -10,7 +10,8 @@
 #   adaptive          Cornell 800^2 spp256 with the reference's adaptive defaults
 #   config5           BASELINE config 5 (spheres-100k 4096^2 spp1024 depth 100)
 #   prof              bench under rocprofv3 --kernel-trace --stats (csv)
-#   valu / traffic    the VALU / HBM counter passes of the bench configs (separate --pmc runs)
+#   valu / traffic    the VALU / HBM counter passes of the bench configs + fp32 + adaptive (separate --pmc runs)
+#   valu5 / traffic5  the same for BASELINE config 5 (spheres-100k 4096^2 spp1024 depth 100, 32 passes)
 #   rankshare         tools/rank_share.py for Cornell and spheres-500
 #   sections          tools/profile_sections.py (section timers of the pool kernel)
 #   bench:<args>      one extra bench line with <args> (underscores become spaces)
@@ -23,6 +24,7 @@ cd $R
 B="python bench.py --no-cpu"
 CFGS4=("" "--scene spheres --spp 64 --depth 8" "--scene rain --width 1920 --spp 512 --depth 16" \
        "--scene spheres100k --width 4096 --spp 16 --depth 100")
+CFG5="--scene spheres100k --width 4096 --spp 1024 --depth 100"
 run() {  # run <seconds> <log> <cmd...>
   local t=$1 log=$2; shift 2
   timeout -k 10 $t "$@" > $O/$log 2>&1
@@ -42,13 +44,15 @@ for step in "$@"; do
       run 300 b_100k.log $B ${CFGS4[3]} --steps 2 --warmup 1 || exit $? ;;
     fp32) run 200 b_cornell_fp32.log $B --precision fp32 --steps 5 --warmup 1 || exit $? ;;
     adaptive) run 300 b_adaptive.log $B --adaptive --steps 3 --warmup 1 || exit $? ;;
-    config5) run 600 b_config5.log $B --scene spheres100k --width 4096 --spp 1024 --depth 100 --steps 1 --warmup 0 --no-count || exit $? ;;
+    config5) run 600 b_config5.log $B $CFG5 --steps 1 --warmup 0 --no-count || exit $? ;;
     bench:*) a=${step#bench:}; run 300 b_extra_$(echo $a | tr -c 'a-z0-9' _ | cut -c1-40).log $B ${a//_/ } || exit $? ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
         --output-format csv -- python3 $R/bench.py --no-cpu > $R/$O/prof.log 2>&1) || exit $? ;;
-    valu) VALU_DIR=$O/valu bash tools/pmc_valu.sh "${CFGS4[@]}" "--precision fp32" || exit $? ;;
-    traffic) bash tools/pmc_traffic.sh "${CFGS4[@]}" && cp -r gpurun_out/traffic $O/ || exit $? ;;
+    valu) VALU_DIR=$O/valu bash tools/pmc_valu.sh "${CFGS4[@]}" "--precision fp32" "--adaptive" || exit $? ;;
+    valu5) VALU_DIR=$O/valu5 bash tools/pmc_valu.sh "$CFG5" || exit $? ;;
+    traffic) TRAFFIC_DIR=$O/traffic bash tools/pmc_traffic.sh "${CFGS4[@]}" "--precision fp32" "--adaptive" || exit $? ;;
+    traffic5) TRAFFIC_DIR=$O/traffic5 bash tools/pmc_traffic.sh "$CFG5" || exit $? ;;
     rankshare)
       run 200 rank_share_cornell.log python tools/rank_share.py cornell || exit $?
       run 200 rank_share_spheres.log python tools/rank_share.py spheres || exit $? ;;
