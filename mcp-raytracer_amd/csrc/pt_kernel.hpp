@@ -59,6 +59,8 @@ struct DevScene {
     int32_t off_tsph;                   // byte offset of tsph in the blob
     int32_t lds_stack_bytes;            // LDS bytes of the traversal stack (scene follows)
     int32_t lds_pool_off;               // pool kernel: byte offset of the per-wave path pools (after the scene)
+    int32_t lds_node_pad;               // LDS copy: one 16-byte pad row after each 4-wide node (t4 nodes, or 0)
+    int32_t t4_stride;                  // bytes between 4-wide nodes where the walk reads them (128 or 144)
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
@@ -652,6 +654,17 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
     return slab_accept(tn, tf, f);
 }
 
+// 4-wide node `ref` where the walk reads it: the blob (global, 128-byte nodes) or the LDS copy,
+// where each node is followed by a 16-byte pad row (scene_prologue). A ds_read_b128 serves 16
+// lanes per LDS cycle, 16 bytes each, from bank (address / 4) mod 64: with 128-byte nodes, row r
+// of node i sits at bank 32 i + 4 r (mod 64), only two bank windows for the 16 lanes reading that
+// row of their (different) nodes - up to 8-way conflicts (spheres-500: 40 % of the LDS-array
+// cycles were bank conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE). At 144 bytes the
+// window is 36 i + 4 r: 16 distinct windows for i mod 16.
+__device__ __forceinline__ const RtT4Node* t4_node(const DevScene& S, int ref) {
+    return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) + (size_t)ref * S.t4_stride);
+}
+
 // One step of the 4-wide walk (RtT4Node) at node `nd`: the slab tests of its four children,
 // the nearest hit child is returned as the next reference and the other hit children are
 // pushed farthest first (so the nearer pop first); with no hit child the next reference is
@@ -963,7 +976,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     // children are pushed farthest first (so the nearer pop first)
     auto node_step = [&](int ref) -> int {
         if (COUNT) cnt[CT_NODE] += 4;
-        return t4_step<kStackStride>(reinterpret_cast<const RtT4Node*>(S.tnodes) + ref, f, thi, stk, sp);
+        return t4_step<kStackStride>(t4_node(S, ref), f, thi, stk, sp);
     };
 #else
     // one node step: the next node / leaf to visit
@@ -1092,7 +1105,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
 #if RT_BVH4
             auto node_step = [&](int ref) -> int {
                 if (COUNT) cnt[CT_NODE] += 4;
-                return t4_step<STRIDE>(reinterpret_cast<const RtT4Node*>(S.tnodes) + ref, f, thi, stk, sp);
+                return t4_step<STRIDE>(t4_node(S, ref), f, thi, stk, sp);
             };
 #else
             auto node_step = [&](int ref) -> int {
@@ -2064,6 +2077,8 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
     if (LDSS > 0) {
         const char* b = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
+        S.t4_stride = S0.lds_node_pad > 0 ? (int)sizeof(RtT4Node) + 16 : (int)sizeof(RtT4Node);
+        b += (size_t)S0.lds_node_pad * 16;  // every section after the nodes moves by the pad rows
         S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
         S.tsph = reinterpret_cast<const float4*>(b + S0.off_tsph);
         S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
@@ -2086,7 +2101,10 @@ template <int LDSS>
 __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
     if (LDSS > 0) {
         uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
-        for (int w = threadIdx.x; w < S0.lds_words; w += blockDim.x) dst[w] = S0.blob[w];
+        // the 4-wide nodes (8 rows each) take a pad row each (t4_node); the rest moves by those rows
+        const int node_rows = S0.lds_node_pad * 8;
+        for (int w = threadIdx.x; w < S0.lds_words; w += blockDim.x)
+            dst[w < node_rows ? w + (w >> 3) : w + S0.lds_node_pad] = S0.blob[w];
         __syncthreads();
     }
     return scene_view<LDSS>(S0, lds_stack);

@@ -293,6 +293,8 @@ struct rt_camera {
         S.off_lights = off_lights;
         S.lds_stack_bytes = 0;
         S.lds_pool_off = 0;
+        S.lds_node_pad = 0;  // set per launch when the scene is LDS-resident
+        S.t4_stride = (int32_t)sizeof(RtT4Node);
         S.troot = RT_BVH4 ? build.t4root : build.troot;
         S.root_box = build.troot_box;
         S.cam = build.cam;
@@ -328,12 +330,17 @@ struct rt_camera {
         // records through scalar loads either way; LDS serves the per-lane
         // reads (hit record, materials, light sampling).
         const size_t lds_cap = (size_t)std::min(lds_max, kLdsSceneMaxBytes);
+        // the LDS copy pads every 4-wide node to 144 bytes (pt_kernel.hpp t4_node: LDS bank windows)
+        const int32_t node_pad =
+            RT_BVH4 && v.trav == TRAV_FAST && env_flag("RT_AMD_NODE_PAD", true) ? (int32_t)build.t4nodes.size() : 0;
         g.lds_level = 0;
         if (lds_scene_enabled() && v.trav != TRAV_REFERENCE) {
-            if (stack + (size_t)lds_words2 * 16 <= lds_cap && env_flag("RT_AMD_LDS_MATS", true)) g.lds_level = 2;
-            else if (v.trav == TRAV_FAST && stack + (size_t)lds_words * 16 <= lds_cap) g.lds_level = 1;
+            if (stack + (size_t)(lds_words2 + node_pad) * 16 <= lds_cap && env_flag("RT_AMD_LDS_MATS", true))
+                g.lds_level = 2;
+            else if (v.trav == TRAV_FAST && stack + (size_t)(lds_words + node_pad) * 16 <= lds_cap)
+                g.lds_level = 1;
         }
-        g.lds_bytes = stack + (size_t)(g.lds_level == 2 ? lds_words2 : g.lds_level == 1 ? lds_words : 0) * 16;
+        g.lds_bytes = stack + (g.lds_level == 0 ? 0 : (size_t)((g.lds_level == 2 ? lds_words2 : lds_words) + node_pad) * 16);
         // Deferred exact sphere tests pay where the walk is VALU-bound and leaves hold
         // several candidates: LDS-resident trees of >= 100 primitives (spheres-500
         // +4.7 %); tiny trees have ~1 candidate per ray (rain-50 -1.3 %) and trees
@@ -359,6 +366,7 @@ struct rt_camera {
         DevScene S = dev_scene();
         S.lds_stack_bytes = (int32_t)stack;
         S.lds_words = g.lds_level == 2 ? lds_words2 : lds_words;
+        S.lds_node_pad = g.lds_level > 0 ? node_pad : 0;
         // Fixed spp: the chunked / pool kernels (per-sample records, in-order accumulate)
         // at every size. Round 1 kept the sequential kernel for images of >= 4 tiles per
         // resident wave; with the hand-out rules above the chunked kernel is faster there

@@ -1342,7 +1342,9 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
         }
     }
     // stack entries: reference DFS (depth + 1), binary fast tree (depth + 1),
-    // 4-wide tree (up to 3 pushes per level + 1)
+    // 4-wide tree (up to 3 pushes per level + 1). The 4-wide node step (pt_kernel.hpp t4_step)
+    // writes up to sp + 2 whatever it pushes: at a node of level L the stack holds at most
+    // 3 (L - 1) entries, so its writes stay below 3 t4depth entries - inside this bound.
     cam.stack_depth = std::max(b.out.bvh_depth, RT_BVH4 ? 3 * b.out.t4depth + 1 : b.out.tdepth) + 1;
     b.out.fast_ok = prims_inside_boxes(b.out.prims);
     return std::move(b.out);
