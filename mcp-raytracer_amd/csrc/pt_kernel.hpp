@@ -1307,13 +1307,25 @@ __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Rea
 // -Q[ib] su, qm = max(|Q[ia]|, |Q[ib]|)}. The plane's t comes from the ray's slab constants,
 // t = fma(x_a, inv[a], noi[a]), instead of a reciprocal of n.d per quad, and alpha / beta are
 // two FMAs each on host-folded products (round 4: 45 -> ~20 VALU per quad).
-// Error: x_a and noi are rounded (the exact test divides D - n.o by n.d in double), and inv is
-// v_rcp's (<= 1 ulp): |t - t_exact| <= ~4u (|x_a inv| + |noi|) + 2^-23 |t| <= kRel (|t| + |noi|),
-// since |x_a inv| <= |t| + |noi| (u = 2^-24, kRel ~ 168 u). The in-plane coordinate
+// Error of t, first order (u = 2^-24): inv = (1/d)(1 + e1), |e1| <= 2u (v_rcp_f32, 1 ulp);
+// noi = -o inv (1 + e2) and x_a = x*(1 + e3), |e2|, |e3| <= u (x* = D / n_a, the exact test's
+// plane); the fma rounds once more (e4). With t* = (x* - o) / d the exact test's t,
+//   t - t* = t* e1 + inv (x* e3 - o e2) + t e4,  |t - t*| <= 2u |t*| + u (|x* inv| + |noi|) + u |t|
+//                                                          <= 2u |noi| + 4u |t|   (|x* inv| <= |t| + |noi|)
+// (the exact test's own double rounding is ~1e-16 relative). kEt = 1e-6 ~ 17u covers each term 4x
+// over. Round 2/3 used kRel = 1e-5 here: a ray leaving a wall at x_a = 555 has |noi| = 555 / |d_a|,
+// so the wall it starts on stayed a candidate (lower bound < 0: tested FIRST) unless |d_a| > 5.5 -
+// never - so it was tested first, and then the wall the ray does hit; at kEt the wall it leaves
+// is rejected whenever |d_a| > ~0.56 (the exact test could only return a self-hit t =
+// (x* - o) / d ~ 3e-5 / |d_a| > 0.001 below |d_a| ~ 0.03). The in-plane coordinate
 // o + t d - Q is off by at most et |d| + a few u (|o| + |t d| + |Q|) <= dp below (|o| <= on,
 // |d| <= dn, |Q| <= qm), times |sv| (|su|) in alpha (beta), plus the 1e-4 absolute that
 // covers alpha's own rounding near [0, 1]. Near-parallel rays (|d[a]| <= 1e-3 |d|, or a ray
 // whose slab constants overflowed: pthr = inf) are decided by the exact test.
+#ifndef RT_KET
+#define RT_KET 1e-6f  // (A/B: 1e-5f = the round-3 margin)
+#endif
+constexpr float kEt = RT_KET;
 template <int CODE>
 __device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, float& lo) {
     RT_FP32_FUSED
@@ -1323,7 +1335,7 @@ __device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, f
     lo = kTminLo;
     if (!(::fabsf(f.d[a]) > f.pthr)) return true;
     const float t = __builtin_fmaf(xa, f.inv[a], f.noi[a]);
-    const float et = kRel * (::fabsf(t) + ::fabsf(f.noi[a])) + 1e-30f;
+    const float et = kEt * (::fabsf(t) + ::fabsf(f.noi[a])) + 1e-30f;
     if (t + et < kTminLo) return false;
     lo = t - et;
     const float alpha = __builtin_fmaf(__builtin_fmaf(t, f.d[ia], f.o[ia]), sv, nq1);
