@@ -61,6 +61,9 @@ struct DevScene {
     int32_t lds_pool_off;               // pool kernel: byte offset of the per-wave path pools (after the scene)
     int32_t lds_node_pad;               // LDS copy: one 16-byte pad row after each 4-wide node (t4 nodes, or 0)
     int32_t t4_stride;                  // bytes between 4-wide nodes where the walk reads them (128 or 144)
+    int32_t n_top;                      // launches walking the tree from global memory: nodes [0, n_top)
+                                        // (breadth-first: the tree's top) have a padded copy in LDS
+    const char* top_lds;                // ... after the traversal stack (scene_view; LDSS 0 only)
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
@@ -661,8 +664,34 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 // row of their (different) nodes - up to 8-way conflicts (spheres-500: 40 % of the LDS-array
 // cycles were bank conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE). At 144 bytes the
 // window is 36 i + 4 r: 16 distinct windows for i mod 16.
+// A launch that walks the tree from global memory (LDSS 0: spheres-100k's 2.8 MB of nodes) keeps
+// the tree's top - the first n_top nodes in breadth-first order, the part every walk starts with -
+// in LDS beside the stack (t4_step reads a node from there or from global memory: two loads in two
+// branches, so each stays a ds_read / global_load - one generic pointer made them flat loads,
+// 3.5 % slower on spheres-100k).
 __device__ __forceinline__ const RtT4Node* t4_node(const DevScene& S, int ref) {
     return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) + (size_t)ref * S.t4_stride);
+}
+struct T4Rows {
+    float4 mn[3], mx[3];
+    int4 rf;
+};
+// A node's 7 rows through a pointer of address space AS (1 global, 3 LDS, 0 generic: whatever the
+// compiler infers): typed loads of distinct address spaces in the two branches of t4_step cannot
+// be merged into one flat load.
+template <int AS>
+__device__ __forceinline__ void t4_rows(const void* nd0, T4Rows& R) {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(AS))) v4* P4;
+    const P4 q = (P4)__builtin_assume_aligned(nd0, 16);
+    auto f4 = [](v4 v) { return make_float4(v.x, v.y, v.z, v.w); };
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        R.mn[a] = f4(q[a]);
+        R.mx[a] = f4(q[3 + a]);
+    }
+    const v4 r = q[6];
+    R.rf = make_int4(__float_as_int(r.x), __float_as_int(r.y), __float_as_int(r.z), __float_as_int(r.w));
 }
 
 // One step of the 4-wide walk (RtT4Node) at node `nd`: the slab tests of its four children,
@@ -682,15 +711,14 @@ __device__ __forceinline__ const RtT4Node* t4_node(const DevScene& S, int ref) {
 //    entries (3 per ancestor), so writes stay below 3 t4depth <= stack_depth - 2 entries
 //    (scene.cpp: stack_depth = max(..., 3 t4depth + 1) + 1).
 template <int STRIDE>
-__device__ __forceinline__ int t4_step(const RtT4Node* nd0, const FRay& f, float thi, int* stk, int& sp) {
-    const RtT4Node* nd = reinterpret_cast<const RtT4Node*>(__builtin_assume_aligned(nd0, 16));
-    const float4 mnx = *reinterpret_cast<const float4*>(nd->bmin[0]);
-    const float4 mny = *reinterpret_cast<const float4*>(nd->bmin[1]);
-    const float4 mnz = *reinterpret_cast<const float4*>(nd->bmin[2]);
-    const float4 mxx = *reinterpret_cast<const float4*>(nd->bmax[0]);
-    const float4 mxy = *reinterpret_cast<const float4*>(nd->bmax[1]);
-    const float4 mxz = *reinterpret_cast<const float4*>(nd->bmax[2]);
-    const int4 rf = *reinterpret_cast<const int4*>(nd->ref);
+__device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f, float thi, int* stk, int& sp) {
+    T4Rows R;
+    if (ref < S.n_top) t4_rows<3>(S.top_lds + (size_t)ref * (sizeof(RtT4Node) + 16), R);
+    else if (S.n_top > 0) t4_rows<1>(t4_node(S, ref), R);  // (LDSS 0: the rest is in global memory)
+    else t4_rows<0>(t4_node(S, ref), R);
+    const float4 mnx = R.mn[0], mny = R.mn[1], mnz = R.mn[2];
+    const float4 mxx = R.mx[0], mxy = R.mx[1], mxz = R.mx[2];
+    const int4 rf = R.rf;
     const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w}, {mnz.x, mnz.y, mnz.z, mnz.w}};
     const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
     const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
@@ -976,7 +1004,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     // children are pushed farthest first (so the nearer pop first)
     auto node_step = [&](int ref) -> int {
         if (COUNT) cnt[CT_NODE] += 4;
-        return t4_step<kStackStride>(t4_node(S, ref), f, thi, stk, sp);
+        return t4_step<kStackStride>(S, ref, f, thi, stk, sp);
     };
 #else
     // one node step: the next node / leaf to visit
@@ -1105,7 +1133,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
 #if RT_BVH4
             auto node_step = [&](int ref) -> int {
                 if (COUNT) cnt[CT_NODE] += 4;
-                return t4_step<STRIDE>(t4_node(S, ref), f, thi, stk, sp);
+                return t4_step<STRIDE>(S, ref, f, thi, stk, sp);
             };
 #else
             auto node_step = [&](int ref) -> int {
@@ -2086,7 +2114,9 @@ __device__ __forceinline__ void publish_counters(const RenderOut& out, const uin
 template <int LDSS>
 __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stack) {
     DevScene S = S0;
+    if (LDSS == 0) S.top_lds = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
     if (LDSS > 0) {
+        S.n_top = 0;  // the whole tree is in LDS (a constant: the walk's reads stay ds_read)
         const char* b = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
         S.tnodes = reinterpret_cast<const RtTNode*>(b);
         S.t4_stride = S0.lds_node_pad > 0 ? (int)sizeof(RtT4Node) + 16 : (int)sizeof(RtT4Node);
@@ -2111,6 +2141,11 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
 // from the global copy.)
 template <int LDSS>
 __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
+    if (LDSS == 0 && S0.n_top > 0) {  // the tree's top: n_top nodes of 8 rows, a pad row each
+        uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
+        for (int w = threadIdx.x; w < S0.n_top * 8; w += blockDim.x) dst[w + (w >> 3)] = S0.blob[w];
+        __syncthreads();
+    }
     if (LDSS > 0) {
         uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
         // the 4-wide nodes (8 rows each) take a pad row each (t4_node); the rest moves by those rows

@@ -295,6 +295,8 @@ struct rt_camera {
         S.lds_pool_off = 0;
         S.lds_node_pad = 0;  // set per launch when the scene is LDS-resident
         S.t4_stride = (int32_t)sizeof(RtT4Node);
+        S.n_top = 0;         // set per launch when the tree is walked from global memory
+        S.top_lds = nullptr;
         S.troot = RT_BVH4 ? build.t4root : build.troot;
         S.root_box = build.troot_box;
         S.cam = build.cam;
@@ -341,6 +343,13 @@ struct rt_camera {
                 g.lds_level = 1;
         }
         g.lds_bytes = stack + (g.lds_level == 0 ? 0 : (size_t)((g.lds_level == 2 ? lds_words2 : lds_words) + node_pad) * 16);
+        // a tree walked from global memory: its top (breadth-first prefix) in the LDS left beside the stack
+        int32_t n_top = 0;
+        if (g.lds_level == 0 && RT_BVH4 && v.trav == TRAV_FAST && lds_scene_enabled() && env_flag("RT_AMD_TOP_CACHE", true)) {
+            const size_t room = lds_cap > stack ? lds_cap - stack : 0;
+            n_top = (int32_t)std::min<size_t>(build.t4nodes.size(), room / (sizeof(RtT4Node) + 16));
+            g.lds_bytes = stack + (size_t)n_top * (sizeof(RtT4Node) + 16);
+        }
         // Deferred exact sphere tests pay where the walk is VALU-bound and leaves hold
         // several candidates: LDS-resident trees of >= 100 primitives (spheres-500
         // +4.7 %); tiny trees have ~1 candidate per ray (rain-50 -1.3 %) and trees
@@ -367,6 +376,7 @@ struct rt_camera {
         S.lds_stack_bytes = (int32_t)stack;
         S.lds_words = g.lds_level == 2 ? lds_words2 : lds_words;
         S.lds_node_pad = g.lds_level > 0 ? node_pad : 0;
+        S.n_top = n_top;
         // Fixed spp: the chunked / pool kernels (per-sample records, in-order accumulate)
         // at every size. Round 1 kept the sequential kernel for images of >= 4 tiles per
         // resident wave; with the hand-out rules above the chunked kernel is faster there

@@ -986,13 +986,41 @@ static int32_t t4_build(const std::vector<RtNode>& f, int32_t i, int depth, std:
     }
     return idx;
 }
+// The 4-wide nodes re-numbered breadth-first (root 0, then its children, ...): any prefix of
+// the array is the top of the tree - the nodes every ray's walk starts with - which a launch
+// walking the tree from global memory copies into LDS (pt_kernel.hpp t4_node). The walk's
+// result does not depend on node numbering (the (t, slot) minimum).
+static std::vector<RtT4Node> t4_breadth_first(const std::vector<RtT4Node>& in) {
+    std::vector<int32_t> order, idx(in.size(), -1);
+    order.reserve(in.size());
+    order.push_back(0);
+    idx[0] = 0;
+    for (size_t h = 0; h < order.size(); ++h)
+        for (int k = 0; k < 4; ++k) {
+            const int32_t r = in[(size_t)order[h]].ref[k];
+            if (r >= 0) {  // interior child (leaf codes and empty slots are negative)
+                idx[(size_t)r] = (int32_t)order.size();
+                order.push_back(r);
+            }
+        }
+    if (order.size() != in.size()) throw std::runtime_error("4-wide tree: unreachable nodes");
+    std::vector<RtT4Node> out(in.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+        RtT4Node n = in[(size_t)order[i]];
+        for (int k = 0; k < 4; ++k)
+            if (n.ref[k] >= 0) n.ref[k] = idx[(size_t)n.ref[k]];
+        out[i] = n;
+    }
+    return out;
+}
+
 std::vector<RtT4Node> make_t4nodes(const std::vector<RtNode>& f, int32_t& root_ref, int& depth) {
     std::vector<RtT4Node> out;
     depth = 0;
     if (f.empty()) { root_ref = ~0; return out; }
     if (f[0].b < 0) { root_ref = t4_leaf_ref(f[0]); return out; }
-    root_ref = t4_build(f, 0, 1, out, depth);
-    return out;
+    root_ref = t4_build(f, 0, 1, out, depth);  // the root is node 0 (pre-order)
+    return t4_breadth_first(out);
 }
 
 // ---------------------------------------------------------------------------
