@@ -64,6 +64,8 @@ struct DevScene {
     int32_t n_top;                      // launches walking the tree from global memory: nodes [0, n_top)
                                         // (breadth-first: the tree's top) have a padded copy in LDS
     const char* top_lds;                // ... after the traversal stack (scene_view; LDSS 0 only)
+    int32_t nearfar;                    // 4-wide node step picks near / far rows by the ray's signs (t4_step);
+                                        // scene_view sets a constant per LDS level (see there)
     int32_t troot;                      // fast traversal root reference
     RtNode root_box;                    // fast traversal root box (padded)
     RtCamera cam;
@@ -374,6 +376,9 @@ constexpr float kRel = 1e-5f;
 #ifndef RT_FUSED_FILTERS
 #define RT_FUSED_FILTERS 1
 #endif
+#ifndef RT_NEARFAR
+#define RT_NEARFAR 1  // 0: rows in node order, near / far planes by min / max (A/B)
+#endif
 #if RT_FUSED_FILTERS
 #define RT_FP32_FUSED _Pragma("clang fp contract(fast)")
 #else
@@ -590,6 +595,7 @@ struct FRay {
     float noi[3];  // -(o * inv): the slab planes' t = fma(b, inv, noi)
     float eps;     // absolute t slack of the fused slab test (>= 2u max|o * inv|, see slab_t)
     float pthr;    // |d[a]| at or below which an axis quad counts as near-parallel (inf: every one)
+    int nrow[3];   // byte offset in a 4-wide node of axis a's near-plane row (bmin[a], or bmax[a] when inv[a] < 0)
     float a;       // |d|^2
     float ia;      // ~1/|d|^2
     float on;      // |o| (rounded up)
@@ -609,6 +615,7 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
         f.inv[a] = __builtin_amdgcn_rcpf(cc);  // <= 1 ulp: a common factor of an axis' two planes
         f.noi[a] = -(f.o[a] * f.inv[a]);
         m = ::fmaxf(m, ::fabsf(f.noi[a]));
+        f.nrow[a] = 16 * a + (RT_NEARFAR && f.inv[a] < 0.0f ? 48 : 0);
     }
     // 1e-6 * max|o * inv| ~ 16 u: covers the rounding of o * inv at both ends of the interval
     f.eps = m * 1e-6f;
@@ -673,24 +680,27 @@ __device__ __forceinline__ const RtT4Node* t4_node(const DevScene& S, int ref) {
     return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) + (size_t)ref * S.t4_stride);
 }
 struct T4Rows {
-    float4 mn[3], mx[3];
+    float4 nr[3], fr[3];  // per axis: the four children's near-plane / far-plane coordinates
     int4 rf;
 };
-// A node's 7 rows through a pointer of address space AS (1 global, 3 LDS, 0 generic: whatever the
+// A node's rows through a pointer of address space AS (1 global, 3 LDS, 0 generic: whatever the
 // compiler infers): typed loads of distinct address spaces in the two branches of t4_step cannot
-// be merged into one flat load.
+// be merged into one flat load. The ray's direction signs pick which row of each axis is the near
+// plane (FRay::nrow): the slab test then needs no min / max per plane pair (below).
 template <int AS>
-__device__ __forceinline__ void t4_rows(const void* nd0, T4Rows& R) {
+__device__ __forceinline__ void t4_rows(const void* nd0, const FRay& f, bool nf, T4Rows& R) {
     typedef float v4 __attribute__((ext_vector_type(4)));
     typedef const __attribute__((address_space(AS))) v4* P4;
-    const P4 q = (P4)__builtin_assume_aligned(nd0, 16);
+    typedef const __attribute__((address_space(AS))) char* PC;
+    const PC b = (PC)__builtin_assume_aligned(nd0, 16);
     auto f4 = [](v4 v) { return make_float4(v.x, v.y, v.z, v.w); };
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        R.mn[a] = f4(q[a]);
-        R.mx[a] = f4(q[3 + a]);
+        const int nrow = nf ? f.nrow[a] : 16 * a;
+        R.nr[a] = f4(*(P4)(b + nrow));
+        R.fr[a] = f4(*(P4)(b + (32 * a + 48 - nrow)));  // the other row of axis a
     }
-    const v4 r = q[6];
+    const v4 r = *(P4)(b + 96);
     R.rf = make_int4(__float_as_int(r.x), __float_as_int(r.y), __float_as_int(r.z), __float_as_int(r.w));
 }
 
@@ -713,27 +723,35 @@ __device__ __forceinline__ void t4_rows(const void* nd0, T4Rows& R) {
 template <int STRIDE>
 __device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f, float thi, int* stk, int& sp) {
     T4Rows R;
-    if (ref < S.n_top) t4_rows<3>(S.top_lds + (size_t)ref * (sizeof(RtT4Node) + 16), R);
-    else if (S.n_top > 0) t4_rows<1>(t4_node(S, ref), R);  // (LDSS 0: the rest is in global memory)
-    else t4_rows<0>(t4_node(S, ref), R);
-    const float4 mnx = R.mn[0], mny = R.mn[1], mnz = R.mn[2];
-    const float4 mxx = R.mx[0], mxy = R.mx[1], mxz = R.mx[2];
-    const int4 rf = R.rf;
-    const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w}, {mnz.x, mnz.y, mnz.z, mnz.w}};
-    const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
-    const int cr[4] = {rf.x, rf.y, rf.z, rf.w};
+    const bool nf = RT_NEARFAR && S.nearfar;
+    if (ref < S.n_top) t4_rows<3>(S.top_lds + (size_t)ref * (sizeof(RtT4Node) + 16), f, nf, R);
+    else if (S.n_top > 0) t4_rows<1>(t4_node(S, ref), f, nf, R);  // (LDSS 0: the rest is in global memory)
+    else t4_rows<0>(t4_node(S, ref), f, nf, R);
+    const float bn[3][4] = {{R.nr[0].x, R.nr[0].y, R.nr[0].z, R.nr[0].w}, {R.nr[1].x, R.nr[1].y, R.nr[1].z, R.nr[1].w},
+                            {R.nr[2].x, R.nr[2].y, R.nr[2].z, R.nr[2].w}};
+    const float bf[3][4] = {{R.fr[0].x, R.fr[0].y, R.fr[0].z, R.fr[0].w}, {R.fr[1].x, R.fr[1].y, R.fr[1].z, R.fr[1].w},
+                            {R.fr[2].x, R.fr[2].y, R.fr[2].z, R.fr[2].w}};
+    const int cr[4] = {R.rf.x, R.rf.y, R.rf.z, R.rf.w};
     uint32_t k[4];
     int r[4];
     int n = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
+        // near / far plane t per axis: the same two values min / max would pick (fma is monotone
+        // in b for a fixed inv, so the sign of inv orders the planes; a NaN plane - an infinite
+        // bound times inv = 0 - is ignored by fmaxf / fminf either way)
         float tn = kTminLo, tf = thi;
+        if (nf) {
+            tn = ::fmaxf(::fmaxf(::fmaxf(slab_t(bn[0][c], f, 0), slab_t(bn[1][c], f, 1)), slab_t(bn[2][c], f, 2)), tn);
+            tf = ::fminf(::fminf(::fminf(slab_t(bf[0][c], f, 0), slab_t(bf[1][c], f, 1)), slab_t(bf[2][c], f, 2)), tf);
+        } else {
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float t0 = slab_t(bmn[a][c], f, a);
-            const float t1 = slab_t(bmx[a][c], f, a);
-            tn = ::fmaxf(tn, ::fminf(t0, t1));
-            tf = ::fminf(tf, ::fmaxf(t0, t1));
+            for (int a = 0; a < 3; ++a) {
+                const float t0 = slab_t(bn[a][c], f, a);
+                const float t1 = slab_t(bf[a][c], f, a);
+                tn = ::fmaxf(tn, ::fminf(t0, t1));
+                tf = ::fminf(tf, ::fmaxf(t0, t1));
+            }
         }
         const bool hit = (cr[c] != kT4Empty) & slab_accept(tn, tf, f);
         k[c] = hit ? __float_as_uint(tn) : ~0u;
@@ -2114,6 +2132,11 @@ __device__ __forceinline__ void publish_counters(const RenderOut& out, const uin
 template <int LDSS>
 __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stack) {
     DevScene S = S0;
+    // near / far rows (t4_step) where the tree is in LDS: spheres-500 +5.3 %, rain +2.8 %; in the
+    // LDSS 0 kernels the three row offsets per ray pushed the chunk kernel from 48 to 88 bytes of
+    // scratch spills and spheres-100k lost 2.3 % (profiles/r04/nearfar/). A constant per level, so
+    // the unused form folds away.
+    S.nearfar = LDSS > 0 ? 1 : 0;
     if (LDSS == 0) S.top_lds = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
     if (LDSS > 0) {
         S.n_top = 0;  // the whole tree is in LDS (a constant: the walk's reads stay ds_read)

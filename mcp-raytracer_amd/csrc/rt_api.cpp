@@ -297,6 +297,7 @@ struct rt_camera {
         S.t4_stride = (int32_t)sizeof(RtT4Node);
         S.n_top = 0;         // set per launch when the tree is walked from global memory
         S.top_lds = nullptr;
+        S.nearfar = 0;       // (scene_view sets it per LDS level)
         S.troot = RT_BVH4 ? build.t4root : build.troot;
         S.root_box = build.troot_box;
         S.cam = build.cam;
