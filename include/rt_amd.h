@@ -249,10 +249,11 @@ int rt_encode_png_device(const uint8_t* d_rgb, int32_t width, int32_t height, vo
 int rt_debug_png_host(const uint8_t* rgb, int32_t width, int32_t height, uint8_t** out, size_t* out_len);
 
 /* generateImageBuffer's core (src/raytracer.ts:39-113): renders the whole frame
- * on the device as `bands` row bands (divideIntoRegions, src/raytracer.ts:185-205;
- * the reference's worker split - the image does not depend on it), merges their
- * RenderStats (RenderStats.merge) into *stats (may be NULL) and returns the PNG
- * encoded on the device (rt_encode_png_device). *out is malloc'ed (rt_free). */
+ * on the device, writes its RenderStats into *stats (may be NULL) and returns the
+ * PNG encoded on the device (rt_encode_png_device). `bands` is the reference's worker
+ * count (divideIntoRegions, src/raytracer.ts:185-205): neither the image nor the
+ * merged stats (RenderStats.merge) depend on it, so the frame is one launch.
+ * *out is malloc'ed (rt_free). */
 int rt_camera_render_png(rt_camera* cam, int32_t bands, rt_render_stats* stats, uint8_t** out, size_t* out_len);
 
 #ifdef __cplusplus

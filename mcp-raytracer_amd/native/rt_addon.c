@@ -237,8 +237,8 @@ static napi_value EncodePng(napi_env env, napi_callback_info info) {
 }
 
 /* renderPng(camera, bands) -> {png: Buffer, stats}: generateImageBuffer's core
- * (src/raytracer.ts:39-113) on the device - the frame rendered as `bands` row
- * bands (the worker split), stats merged (RenderStats.merge), the PNG encoded on
+ * (src/raytracer.ts:39-113) on the device - `bands` is the reference's worker split
+ * (the frame and its merged stats do not depend on it: one launch), the PNG encoded on
  * the GPU (rt_camera_render_png) so only the compressed file crosses PCIe. */
 static napi_value RenderPng(napi_env env, napi_callback_info info) {
     size_t argc = 2;

@@ -147,8 +147,8 @@ class Camera:
 
     def render_png(self, bands: int = 1):
         """generateImageBuffer's core on the device (rt_camera_render_png): the frame
-        rendered as `bands` row bands (divideIntoRegions; the image does not depend
-        on the split), stats merged, PNG encoded on the GPU -> (png bytes, RenderStats)."""
+        rendered in one launch (`bands`, the reference's worker count, changes neither
+        the image nor the merged stats), PNG encoded on the GPU -> (png bytes, RenderStats)."""
         out, n = C.c_void_p(), C.c_size_t()
         st = _lib.RtRenderStats()
         _lib.check(self._lib.rt_camera_render_png(self._h, int(bands), C.byref(st), C.byref(out), C.byref(n)))

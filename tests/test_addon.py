@@ -70,7 +70,7 @@ def test_addon_render_matches_python_binding(rt, addon, gpu, tmp_path):
     assert np.array_equal(got, ref)
     from raytracer_amd.png import decode_png_rgb
     assert decode_png_rgb(Path(str(out_bin) + ".png").read_bytes()) == (W, H, ref.tobytes())
-    # renderPng: rendered in 3 bands and encoded on the device, merged stats
+    # renderPng (bands 3: the reference's worker count): encoded on the device, the frame's stats
     assert decode_png_rgb(Path(str(out_bin) + ".dev.png").read_bytes()) == (W, H, ref.tobytes())
     assert res["devStats"]["pixels"] == st.pixels and res["devStats"]["samples"]["total"] == st.samples["total"]
     assert sum(s["pixels"] for s in res["stats"]) == st.pixels
