@@ -436,16 +436,21 @@ struct rt_camera {
             // rank shares N=2 3.54 -> 3.27, N=4 2.04 -> 1.78, N=8 1.21 -> 1.03 ms; rain-50 1080p
             // spp512 rank shares N=2 31.5 -> 22.2 ms, N=8 7.8 -> 5.8 ms; profiles/r02/sched/).
             // Trees walked from global memory (a sample costs ~150 us of a lane at config 5) cap
-            // the first chunk at 4 (config 5, 4096^2 spp1024: 9617 -> 8980 ms per frame).
+            // the first chunk at 4 (config 5, 4096^2 spp1024: 9617 -> 8980 ms per frame; 2 since round 4).
             const bool bvh = v.trav == TRAV_FAST;
             // (pool kernel, re-tuned at 152 slots per wave: 8 tile-chunks per atomic from 512 spl,
             // 4 from 48, 2 from 24, first items of at most 4 samples - Cornell N=1 14.61 -> 14.43 ms,
             // 1/2 share 7.57 -> 7.40, 1/8 share 2.57 -> 2.10 ms; profiles/r02/sched/)
+            // (trees walked from global memory, round 4: 8 tile-chunks per atomic from 1024 spl,
+            // chunks of at most 2 samples and shading from 40 walks done, not 48 - config 5's 1/8
+            // share 1070.8 -> 1045.0 ms, spheres-100k 4096^2 spp16 N=1 134.9 -> 131.4 ms;
+            // profiles/r04/cfg5/)
+            const bool gtree = bvh && g.lds_level == 0;
             const int pool_auto = v.pool ? (spl >= 512.0 ? 8 : spl >= 48.0 ? 4 : spl >= 24.0 ? 2 : 1)
-                                 : bvh ? (spl >= 256.0 ? 4 : 2)
+                                 : bvh ? (gtree && spl >= 1024.0 ? 8 : spl >= 256.0 ? 4 : 2)
                                        : (v.trav == TRAV_BRUTE && spl >= 512.0 ? 2 : 1);
             sb.pool = kWave * env_int("RT_AMD_POOL", pool_auto);
-            const int c_max = v.pool ? 4 : (bvh && g.lds_level == 0) ? 4 : 32;
+            const int c_max = v.pool ? 4 : gtree ? 2 : 32;
             // (pool kernel, fixed spp, re-checked at the round-3 build: first items of spl / 64, so 4
             // samples for the whole frame and a 1/2 share, 2 for a 1/4 share, 1 for a 1/8 share -
             // Cornell 1/8 share 2.248 -> 2.051 ms, 1/4 3.998 -> 3.931 ms, N=1 and 1/2 unchanged;
@@ -490,7 +495,7 @@ struct rt_camera {
             if (covered != nsamp) throw std::runtime_error("guided schedule: coverage");
             for (int p = 0; p < np; ++p) sb.rnch[p] = 1.0 / (double)sb.nch[p];
             sb.refill_min = std::min(env_int("RT_AMD_REFILL", 4), kWave);
-            sb.min_ready = std::min(env_int("RT_AMD_READY", 48), kWave);
+            sb.min_ready = std::min(env_int("RT_AMD_READY", gtree ? 40 : 48), kWave);
         };
         // one pass of the path kernel over sb.slots slots (items numbered phase by phase)
         int pass = 0;

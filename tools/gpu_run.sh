@@ -13,7 +13,9 @@
 #   valu / traffic    the VALU / HBM counter passes of the bench configs + fp32 + adaptive (separate --pmc runs)
 #   valu5 / traffic5  the same for BASELINE config 5 (spheres-100k 4096^2 spp1024 depth 100, 32 passes)
 #   rankshare         tools/rank_share.py for Cornell and spheres-500
-#   sections          tools/profile_sections.py (section timers of the pool kernel)
+#   sections          tools/profile_sections.py (section timers of the chunked / sequential kernels)
+#   poolsections      the same for the pool kernel (variant library 'poolprof': RT_POOL_PROF=1, RT_POOL_K=146)
+#   countexact        tools/count_exact.py (exact tests per ray / per wave-trip)
 #   bench:<args>      one extra bench line with <args> (underscores become spaces)
 # Every GPU step runs under its own time limit; the first failing step ends the script.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -57,6 +59,8 @@ for step in "$@"; do
       run 200 rank_share_cornell.log python tools/rank_share.py cornell || exit $?
       run 200 rank_share_spheres.log python tools/rank_share.py spheres || exit $? ;;
     sections) run 300 sections.log python tools/profile_sections.py || exit $? ;;
+    poolsections) RT_AMD_VARIANT=poolprof run 300 sections_pool.log python tools/profile_sections.py cornell || exit $? ;;
+    countexact) run 300 count_exact.log python tools/count_exact.py || exit $? ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done

@@ -3,7 +3,7 @@
 path-kernel ms from HIP events (median of 5 after 2 warm-up renders) per arm.
 Arms come from $ARMS, one per line: "<name> [KEY=VALUE ...]" (env knobs read at
 each launch, e.g. RT_AMD_READY, RT_AMD_POOL, RT_AMD_CHUNK, RT_AMD_REFILL).
-usage: ARMS=... SWEEP_N="1 8" python tools/knob_sweep.py <scene>"""
+usage: ARMS=... SWEEP_N="1 8" [SWEEP_SPP=32] python tools/knob_sweep.py <scene>"""
 import json
 import os
 import sys
@@ -14,7 +14,8 @@ sys.path.insert(0, str(ROOT / "mcp-raytracer_amd"))
 sys.path.insert(0, str(ROOT))
 
 RO = {"cornell": {"width": 800, "samples": 256, "depth": 16}, "spheres": {"width": 800, "samples": 64, "depth": 8},
-      "rain": {"width": 1920, "samples": 512, "depth": 16}}
+      "rain": {"width": 1920, "samples": 512, "depth": 16},
+      "spheres100k": {"width": 4096, "samples": 16, "depth": 100}}
 
 
 def main():
@@ -24,7 +25,10 @@ def main():
     from bench import SCENES
     scene = sys.argv[1]
     cfg, ex, _ = SCENES[scene]
-    cam = rt.create_camera_from_scene_data(rt.generate_scene_data(cfg), {**RO[scene], **ex, "aTolerance": 0})
+    ro = dict(RO[scene])
+    if os.environ.get("SWEEP_SPP"):  # e.g. 32: one pass of config 5 (spp 1024 in passes of 32)
+        ro["samples"] = int(os.environ["SWEEP_SPP"])
+    cam = rt.create_camera_from_scene_data(rt.generate_scene_data(cfg), {**ro, **ex, "aTolerance": 0})
     frame = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     arms = [ln.split() for ln in os.environ.get("ARMS", "base").splitlines() if ln.strip()]
