@@ -168,6 +168,11 @@ int rt_debug_world_hit(rt_camera* cam, int32_t traversal, int32_t n, const float
  * and Math.pow(xi, 5) (Schlick) for xi = u[k] / 2^32: out = host double[3*n]. */
 int rt_debug_math(int32_t n, const uint32_t* u, double* out);
 
+/* The device's restricted-domain double square root and reciprocal beside the general
+ * ones, for x = host double[n]: out = host double[4*n] = {sqrt_rn(x), sqrt(x), rcp_rn(x),
+ * 1 / x} (pins rt_math.hpp sqrt_rn / rcp_rn bit for bit on their domains). */
+int rt_debug_fp64(int32_t n, const double* x, double* out);
+
 /* The path RNG stream (seeded Math.random replacement), host evaluation. */
 int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out);
 

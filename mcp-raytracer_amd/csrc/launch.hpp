@@ -60,6 +60,7 @@ hipError_t launch_world_hit_ref(const DevScene& S, int trav, int n, const float*
 
 // Device transcendental probe (V8 fixture tests): out[3k..3k+2] = cos, sin of 2 pi xi, pow(xi, 5).
 hipError_t launch_math_probe(int n, const uint32_t* u, double* out, hipStream_t stream);
+hipError_t launch_fp64_probe(int n, const double* x, double* out, hipStream_t stream);
 
 // Scatter of tile-packed slabs into the full-frame layout (frame.hip).
 hipError_t launch_tiles_unpack(const void* slabs, int groups, int slab_tiles, const RtRegion& reg, int width,

@@ -224,6 +224,10 @@ __device__ __forceinline__ double m_abs(double x) { return ::fabs(x); }
 __device__ __forceinline__ float m_abs(float x) { return ::fabsf(x); }
 __device__ __forceinline__ double m_sqrt(double x) { return ::sqrt(x); }
 __device__ __forceinline__ float m_sqrt(float x) { return ::sqrtf(x); }
+// The square root of an argument known to be 0 or >= 2^-767 (rt_math.hpp sqrt_rn's domain):
+// a uniform draw r or 1 - r (multiples of 2^-32 below 1), or |1 - x| for a double x.
+__device__ __forceinline__ double m_sqrt_nz(double x) { return RT_FP64_SHORT ? sqrt_rn(x) : ::sqrt(x); }
+__device__ __forceinline__ float m_sqrt_nz(float x) { return ::sqrtf(x); }
 
 template <class Real> struct K {
     static constexpr Real PI = (Real)3.141592653589793;
@@ -777,6 +781,15 @@ __device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f
 }
 
 // fp32 pre-filters: false only when the exact test surely gives no t <= thi.
+// The sphere roots' absolute error bound, kRel (|oc| |d| + |b| + sq) / a (+ a denormal floor),
+// with |oc| |d| bounded without a square root (round 4: one v_sqrt fewer per test): a |oc|^2 =
+// b^2 - disc + a r^2, and the exact disc >= -2 tol once the computed one passed -tol (its
+// rounding is far below tol), so |oc| |d| <= |b| + |d| r + sqrt(2 tol) <= |b| + dn r + 1.5 sq
+// (sq >= sqrt(tol)); the bound used, kRel (2 |b| + dn r + 3 sq) / a, is never smaller.
+__device__ __forceinline__ float sphere_et(float b, float r, float sq, const FRay& f) {
+    RT_FP32_FUSED
+    return kRel * (2.0f * ::fabsf(b) + f.dn * r + 3.0f * sq) * f.ia + 1e-30f;
+}
 __device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi, float& lo) {
     RT_FP32_FUSED
     const float ox = f.o[0] - g.x, oy = f.o[1] - g.y, oz = f.o[2] - g.z;  // = the reference's oc
@@ -789,7 +802,7 @@ __device__ __forceinline__ bool sphere_maybe(float4 g, const FRay& f, float thi,
     const float tol = 4.0f * kRel * f.a * (oo + r * r) + 1e-30f;
     if (disc < -tol) return false;
     const float sq = __builtin_amdgcn_sqrtf(::fmaxf(disc, 0.0f) + tol) * (1.0f + kRel);
-    const float et = kRel * (__builtin_amdgcn_sqrtf(oo * f.a) + ::fabsf(b) + sq) * f.ia + 1e-30f;
+    const float et = sphere_et(b, r, sq, f);
     if ((-b + sq) * f.ia * (1.0f + kRel) + et < kTminLo) return false;
     const float r1 = (-b - sq) * f.ia;
     lo = r1 - ::fabsf(r1) * kRel - et;  // <= the first root; the second is larger
@@ -811,7 +824,7 @@ __device__ __forceinline__ bool sphere_maybe_hi(float4 g, const FRay& f, float t
     const float tol = 4.0f * kRel * f.a * (oo + r * r) + 1e-30f;
     if (disc < -tol) return false;
     const float sq = __builtin_amdgcn_sqrtf(::fmaxf(disc, 0.0f) + tol) * (1.0f + kRel);
-    const float et = kRel * (__builtin_amdgcn_sqrtf(oo * f.a) + ::fabsf(b) + sq) * f.ia + 1e-30f;
+    const float et = sphere_et(b, r, sq, f);
     const float hi2 = (-b + sq) * f.ia * (1.0f + kRel) + et;  // >= every root
     if (hi2 < kTminLo) return false;
     const float r1 = (-b - sq) * f.ia;
@@ -1349,46 +1362,60 @@ __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Rea
     return true;
 }
 
-// The brute-force pass's axis-quad pre-filter over an RtPre record {x_a, sv, su, -Q[ia] sv,
-// -Q[ib] su, qm = max(|Q[ia]|, |Q[ib]|)}. The plane's t comes from the ray's slab constants,
-// t = fma(x_a, inv[a], noi[a]), instead of a reciprocal of n.d per quad, and alpha / beta are
-// two FMAs each on host-folded products (round 4: 45 -> ~20 VALU per quad).
+// The brute-force pass's axis-quad pre-filter over an RtPre record {x_a, sv, su, -Q[ia] sv - 1/2,
+// -Q[ib] su - 1/2, kRel qm} (qm = max(|Q[ia]|, |Q[ib]|)). The plane's t comes from the ray's slab
+// constants, t = fma(x_a, inv[a], noi[a]), instead of a reciprocal of n.d per quad, and alpha - 1/2,
+// beta - 1/2 are two FMAs each on host-folded products (round 4: 45 -> ~16 VALU per quad).
 // Error of t, first order (u = 2^-24): inv = (1/d)(1 + e1), |e1| <= 2u (v_rcp_f32, 1 ulp);
 // noi = -o inv (1 + e2) and x_a = x*(1 + e3), |e2|, |e3| <= u (x* = D / n_a, the exact test's
 // plane); the fma rounds once more (e4). With t* = (x* - o) / d the exact test's t,
 //   t - t* = t* e1 + inv (x* e3 - o e2) + t e4,  |t - t*| <= 2u |t*| + u (|x* inv| + |noi|) + u |t|
 //                                                          <= 2u |noi| + 4u |t|   (|x* inv| <= |t| + |noi|)
-// (the exact test's own double rounding is ~1e-16 relative). kEt = 1e-6 ~ 17u covers each term 4x
-// over. Round 2/3 used kRel = 1e-5 here: a ray leaving a wall at x_a = 555 has |noi| = 555 / |d_a|,
-// so the wall it starts on stayed a candidate (lower bound < 0: tested FIRST) unless |d_a| > 5.5 -
-// never - so it was tested first, and then the wall the ray does hit; at kEt the wall it leaves
-// is rejected whenever |d_a| > ~0.56 (the exact test could only return a self-hit t =
-// (x* - o) / d ~ 3e-5 / |d_a| > 0.001 below |d_a| ~ 0.03). The in-plane coordinate
-// o + t d - Q is off by at most et |d| + a few u (|o| + |t d| + |Q|) <= dp below (|o| <= on,
-// |d| <= dn, |Q| <= qm), times |sv| (|su|) in alpha (beta), plus the 1e-4 absolute that
-// covers alpha's own rounding near [0, 1]. Near-parallel rays (|d[a]| <= 1e-3 |d|, or a ray
-// whose slab constants overflowed: pthr = inf) are decided by the exact test.
+// (the exact test's own double rounding is ~1e-16 relative). et = kEt (|t| + |noi|), kEt = 1e-6
+// ~ 17u, covers each term 4x over. Round 2/3 used kRel = 1e-5 here: a ray leaving a wall at
+// x_a = 555 has |noi| = 555 / |d_a|, so the wall it starts on stayed a candidate (lower bound
+// < 0: tested FIRST) unless |d_a| > 5.5 - never - so it was tested first, and then the wall the
+// ray does hit; at kEt the wall it leaves is rejected whenever |d_a| > ~0.56 (the exact test
+// could only return a self-hit t = (x* - o) / d ~ 3e-5 / |d_a| > 0.001 below |d_a| ~ 0.03).
+// The in-plane coordinate o + t d - Q is off by at most et |d| + a few u (|o| + |t d| + |Q|),
+// which dp = (|t| + |noi|) c1 + c0 + kRel qm bounds (c1 = (kEt + kRel) dn, c0 = kRel on +
+// 1e-30 dn: QuadPreRay; |o| <= on, |d| <= dn, |Q| <= qm), times |sv| (|su|) in alpha (beta).
+// The window test alpha in [-ea, 1 + ea], ea = |sv| dp + 1e-4 (the absolute part covers alpha's
+// own rounding near [0, 1], and the host's folding of the 1/2), is |alpha - 1/2| - |sv| dp <=
+// 1/2 + 1e-4, one FMA with source modifiers, compared against kWin (1e-6 more for that FMA's own
+// rounding); a NaN passes. Near-parallel rays (|d[a]| <= 1e-3 |d|, or a ray whose slab constants
+// overflowed: pthr = inf) are decided by the exact test.
 #ifndef RT_KET
 #define RT_KET 1e-6f  // (A/B: 1e-5f = the round-3 margin)
 #endif
 constexpr float kEt = RT_KET;
+constexpr float kWin = 0.5f + 1e-4f + 1e-6f;
+struct QuadPreRay {
+    float c1, c0;
+};
+__device__ __forceinline__ QuadPreRay quad_pre_ray(const FRay& f) {
+    RT_FP32_FUSED
+    return QuadPreRay{(kEt + kRel) * f.dn, kRel * f.on + 1e-30f * f.dn};
+}
 template <int CODE>
-__device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, float& lo) {
+__device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, const QuadPreRay& qr, float& lo) {
     RT_FP32_FUSED
     constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
     constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
-    const float xa = v[0], sv = v[1], su = v[2], nq1 = v[3], nq2 = v[4], qm = v[5];
+    const float xa = v[0], sv = v[1], su = v[2], nq1 = v[3], nq2 = v[4], qk = v[5];
     lo = kTminLo;
     if (!(::fabsf(f.d[a]) > f.pthr)) return true;
     const float t = __builtin_fmaf(xa, f.inv[a], f.noi[a]);
-    const float et = kEt * (::fabsf(t) + ::fabsf(f.noi[a])) + 1e-30f;
+    const float tn = ::fabsf(t) + ::fabsf(f.noi[a]);
+    const float et = __builtin_fmaf(kEt, tn, 1e-30f);
     if (t + et < kTminLo) return false;
     lo = t - et;
-    const float alpha = __builtin_fmaf(__builtin_fmaf(t, f.d[ia], f.o[ia]), sv, nq1);
-    const float beta = __builtin_fmaf(__builtin_fmaf(t, f.d[ib], f.o[ib]), su, nq2);
-    const float dp = et * f.dn + kRel * (f.on + ::fabsf(t) * f.dn + qm);
-    const float ea = ::fabsf(sv) * dp + 1e-4f, eb = ::fabsf(su) * dp + 1e-4f;
-    return !(alpha < -ea || alpha > 1.0f + ea || beta < -eb || beta > 1.0f + eb);
+    const float alpha = __builtin_fmaf(__builtin_fmaf(t, f.d[ia], f.o[ia]), sv, nq1);  // alpha - 1/2
+    const float beta = __builtin_fmaf(__builtin_fmaf(t, f.d[ib], f.o[ib]), su, nq2);   // beta - 1/2
+    const float dp = __builtin_fmaf(tn, qr.c1, qr.c0 + qk);
+    const float wa = __builtin_fmaf(-::fabsf(sv), dp, ::fabsf(alpha));
+    const float wb = __builtin_fmaf(-::fabsf(su), dp, ::fabsf(beta));
+    return !(wa > kWin) && !(wb > kWin);
 }
 
 // The brute-force pass's per-lane candidate bounds live in fp16 LDS columns (half the
@@ -1415,6 +1442,7 @@ template <class Real, bool COUNT, class Hook = NoHook>
 __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
                                                     uint16_t* lot, uint32_t* cnt, Hook after_prefilter = Hook()) {
     const FRay f = make_fray(r.o, r.d);
+    const QuadPreRay qr = quad_pre_ray(f);
     uint32_t mask = 0u;
     for (int k = 0; k < n_prims; ++k) {
         const RtPre q = ld_uniform(S.gpre, k);  // one scalar load (wave-uniform)
@@ -1427,12 +1455,12 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
             if (COUNT) cnt[CT_QUAD]++;
             const float* v = q.f;
             switch (q.kind) {
-                case 1: maybe = aquad_maybe_pre<1>(v, f, lo); break;
-                case 2: maybe = aquad_maybe_pre<2>(v, f, lo); break;
-                case 3: maybe = aquad_maybe_pre<3>(v, f, lo); break;
-                case 4: maybe = aquad_maybe_pre<4>(v, f, lo); break;
-                case 5: maybe = aquad_maybe_pre<5>(v, f, lo); break;
-                default: maybe = aquad_maybe_pre<6>(v, f, lo); break;
+                case 1: maybe = aquad_maybe_pre<1>(v, f, qr, lo); break;
+                case 2: maybe = aquad_maybe_pre<2>(v, f, qr, lo); break;
+                case 3: maybe = aquad_maybe_pre<3>(v, f, qr, lo); break;
+                case 4: maybe = aquad_maybe_pre<4>(v, f, qr, lo); break;
+                case 5: maybe = aquad_maybe_pre<5>(v, f, qr, lo); break;
+                default: maybe = aquad_maybe_pre<6>(v, f, qr, lo); break;
             }
         } else {
             maybe = prim_maybe<COUNT>(ld_uniform(S.gprims, k), f, lo, cnt);
@@ -1534,7 +1562,7 @@ __device__ __forceinline__ V3 dielectric_dir(Real ior, bool front, V3 din, V3 n,
     if (refl) return reflect<Real>(ud, n);
     // Vec3.refract (src/geometry/vec3.ts:193-209)
     const V3 perp = scale<Real>(add(ud, scale<Real>(n, cosT)), ratio);
-    const V3 par = scale<Real>(n, -m_sqrt(m_abs((Real)1 - len2<Real>(perp))));
+    const V3 par = scale<Real>(n, -m_sqrt_nz(m_abs((Real)1 - len2<Real>(perp))));
     return add(perp, par);
 }
 
@@ -1947,10 +1975,10 @@ __device__ __forceinline__ bool shade_diffuse(const DevScene& S, const RtCamera&
         const Real r1 = uniform<Real>(P.rng);
         const Real r2 = uniform<Real>(P.rng);
         const Real phi = (Real)2 * K<Real>::PI * r1;
-        const Real sr2 = m_sqrt(r2);
+        const Real sr2 = m_sqrt_nz(r2);
         Real sn, cs;
         m_sincos(phi, sn, cs);
-        gdir = onb_local<Real>(b, mk<Real>(cs * sr2, sn * sr2, m_sqrt((Real)1 - r2)));
+        gdir = onb_local<Real>(b, mk<Real>(cs * sr2, sn * sr2, m_sqrt_nz((Real)1 - r2)));
     } else {
         int pick = C.n_lights - 1;
         for (int l = 0; l < C.n_lights; ++l) {

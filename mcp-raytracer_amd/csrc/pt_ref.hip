@@ -287,6 +287,22 @@ __global__ void math_probe_kernel(int n, const uint32_t* u, double* out) {
     out[3 * k + 2] = pow5(xi);
 }
 
+// rt_debug_fp64: the restricted-domain sqrt / reciprocal (rt_math.hpp) beside the general ones
+__global__ void fp64_probe_kernel(int n, const double* x, double* out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double v = x[k];
+    out[4 * k] = sqrt_rn(v);
+    out[4 * k + 1] = ::sqrt(v);
+    out[4 * k + 2] = rcp_rn(v);
+    out[4 * k + 3] = 1.0 / v;
+}
+hipError_t launch_fp64_probe(int n, const double* x, double* out, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fp64_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n, x, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_math_probe(int n, const uint32_t* u, double* out, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n, u, out);

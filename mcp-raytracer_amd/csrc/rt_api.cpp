@@ -191,9 +191,10 @@ struct rt_camera {
                 q.f[0] = (float)(p.s0 / (double)p.g3[a]);          // the plane x_a = D / n_a
                 q.f[1] = (float)asv;
                 q.f[2] = (float)asu;
-                q.f[3] = (float)(-(double)p.g0[ia] * asv);
-                q.f[4] = (float)(-(double)p.g0[ib] * asu);
-                q.f[5] = std::max(std::fabs(p.g0[ia]), std::fabs(p.g0[ib]));
+                q.f[3] = (float)(-(double)p.g0[ia] * asv - 0.5);  // alpha - 1/2 at the quad's corner
+                q.f[4] = (float)(-(double)p.g0[ib] * asu - 0.5);
+                constexpr double kRelPre = 1e-5;  // pt_kernel.hpp kRel
+                q.f[5] = (float)(kRelPre * std::max(std::fabs((double)p.g0[ia]), std::fabs((double)p.g0[ib])) * (1.0 + 1e-6));
                 q.f[6] = 0.0f;
             } else {
                 q.kind = PRE_OTHER;
@@ -992,6 +993,27 @@ int rt_debug_math(int32_t n, const uint32_t* u, double* out) {
         return RT_OK;
     } catch (const std::exception& e) {
         if (d_u) (void)hipFree(d_u);
+        if (d_out) (void)hipFree(d_out);
+        return set_error(RT_ERR_DEVICE, e.what());
+    }
+}
+
+int rt_debug_fp64(int32_t n, const double* x, double* out) {
+    if (n < 0 || (n > 0 && (!x || !out))) return set_error(RT_ERR_INVALID, "bad arguments");
+    double* d_x = nullptr;
+    double* d_out = nullptr;
+    try {
+        if (n == 0) return RT_OK;
+        hip_check(hipMalloc(&d_x, (size_t)n * sizeof(double)), "hipMalloc");
+        hip_check(hipMalloc(&d_out, (size_t)n * 4 * sizeof(double)), "hipMalloc");
+        hip_check(hipMemcpy(d_x, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+        hip_check(launch_fp64_probe(n, d_x, d_out, nullptr), "fp64_probe_kernel");
+        hip_check(hipMemcpy(out, d_out, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+        (void)hipFree(d_x);
+        (void)hipFree(d_out);
+        return RT_OK;
+    } catch (const std::exception& e) {
+        if (d_x) (void)hipFree(d_x);
         if (d_out) (void)hipFree(d_out);
         return set_error(RT_ERR_DEVICE, e.what());
     }

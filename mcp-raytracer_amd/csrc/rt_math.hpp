@@ -52,9 +52,73 @@ template <class Real>
 RT_HD V3 scale(V3 a, Real t) {
     return V3{(float)((Real)a.x * t), (float)((Real)a.y * t), (float)((Real)a.z * t)};
 }
+#ifndef RT_FP64_SHORT
+#define RT_FP64_SHORT 1  // 0: the A/B arm with the general expansions everywhere
+#endif
+#if defined(__HIPCC__)
+// Correctly rounded double sqrt and reciprocal on a restricted domain, bit-identical there to the
+// compiler's general expansions (gfx950), which are the same instruction sequences plus range
+// scaling steps that are the identity on these inputs (round 4: 5 and 4 instructions fewer,
+// 2 and 4 of them fp64):
+//  * sqrt_rn: v_rsq_f64 then the Goldschmidt / Newton steps (h = y/2, r = 1/2 - h g, g += g r,
+//    h += h r, two d = x - g^2, g += d h corrections) and the +-0 / +inf class select. The
+//    general expansion first scales x < 2^-767 by 2^256 (and the root back by 2^-128): valid
+//    for x >= 2^-767, 0, +inf (NaN and x < 0 give NaN either way).
+//  * rcp_rn: the division sequence 1 / y with numerator 1 (div_scale leaves 2^-767 <= |y| <
+//    2^1022 unscaled and sets no post-scale flag, the numerator's product 1 * r is exact,
+//    div_fmas is then a plain fma and div_fixup the identity on the finite non-zero quotient):
+//    v_rcp_f64, two Newton steps, one residual correction. Valid for 2^-767 <= |y| < 2^1022.
+// tests/test_gpu_parity.py checks both against ::sqrt and 1.0 / y on the device (rt_debug_math).
+__device__ __forceinline__ double sqrt_rn(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return __builtin_amdgcn_class(x, 0x260) ? x : g;  // +-0, +inf
+}
+__device__ __forceinline__ double rcp_rn(double y) {
+    const double r0 = __builtin_amdgcn_rcp(y);
+    const double e0 = __builtin_fma(-y, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-y, r1, 1.0);
+    const double r2 = __builtin_fma(r1, e1, r1);
+    const double e2 = __builtin_fma(-y, r2, 1.0);
+    return __builtin_fma(e2, r2, r2);
+}
+__device__ __forceinline__ bool rcp_rn_ok(double y) {
+    const double a = __builtin_fabs(y);
+    return a >= 0x1p-767 && a < 0x1p1022;
+}
+#endif
+// RN(1 / t), the reference's division by a JS number
+template <class Real>
+RT_HD Real recip(Real t) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(Real) == 8 && RT_FP64_SHORT)
+        if (rcp_rn_ok(t)) return rcp_rn(t);
+#endif
+    return (Real)1 / t;
+}
+// RN(1 / RN(sqrt(l))) for l > 0 a sum of squares of fp32 values: l >= 2^-298 (sqrt_rn's domain),
+// and below 2^300 its root is in rcp_rn's (else l is infinite, or NaN).
+template <class Real>
+RT_HD Real rsqrt_rn(Real l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(Real) == 8 && RT_FP64_SHORT)
+        if (l < 0x1p300) return rcp_rn(sqrt_rn(l));
+#endif
+    return (Real)1 / sqrt(l);
+}
+
 // Vec3.divide(t) = vec3.scale(out, a, 1/t) (src/geometry/vec3.ts:126-130).
 template <class Real>
-RT_HD V3 divs(V3 a, Real t) { return scale<Real>(a, (Real)1 / t); }
+RT_HD V3 divs(V3 a, Real t) { return scale<Real>(a, recip<Real>(t)); }
 
 // Vec3.dot / lengthSquared (src/geometry/vec3.ts:132-136,152-157).
 // In double each product of two fp32 values is exact, so fma(y1, y2, x1*x2) =
@@ -90,7 +154,7 @@ RT_HD V3 cross(V3 a, V3 b) {
 template <class Real>
 RT_HD V3 unit(V3 a) {
     Real l = dot<Real>(a, a);
-    if (l > (Real)0) l = (Real)1 / sqrt(l);
+    if (l > (Real)0) l = rsqrt_rn<Real>(l);
     return V3{(float)((Real)a.x * l), (float)((Real)a.y * l), (float)((Real)a.z * l)};
 }
 

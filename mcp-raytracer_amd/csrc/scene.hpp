@@ -99,7 +99,7 @@ static_assert(sizeof(RtMat) == 64, "RtMat must be 64 bytes");
 // fp32 pre-filter of a sphere or an axis-aligned quad reads, in one 32-byte scalar
 // load (the full RtPrim takes two dependent loads for a quad: its type, then its
 // axis code). kind: PRE_SPHERE {cx, cy, cz, r}; 1..6 = axis code {x_a of the plane (D / n[a]),
-// sv = +-w[a]*v[iv], su = +-w[a]*u[iu], -Q[ia]*sv, -Q[ib]*su, max(|Q[ia]|, |Q[ib]|), 0}
+// sv = +-w[a]*v[iv], su = +-w[a]*u[iu], -Q[ia]*sv - 1/2, -Q[ib]*su - 1/2, kRel max(|Q[ia]|, |Q[ib]|), 0}
 // (scene.cpp encode_axis_quad, rt_api.cpp prefilter_records); PRE_OTHER: read the RtPrim.
 enum : int32_t { PRE_SPHERE = 0, PRE_OTHER = 7 };
 struct alignas(16) RtPre {

@@ -86,6 +86,7 @@ _SIGS = {
     "rt_debug_world_hit": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_void_p]),
     "rt_debug_math": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
+    "rt_debug_fp64": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "rt_camera_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "rt_camera_adaptive_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]),

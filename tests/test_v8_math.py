@@ -66,3 +66,46 @@ def test_device_transcendentals_agree_with_v8_and_oracle(rt, oracle, gpu):
     orc = oracle.math_probe(u)
     print("device vs oracle raw differences:", int((dev != orc).any(axis=1).sum()), "of", u.size)
     assert np.array_equal(dev[:, 2], orc[:, 2])  # both the correctly rounded x^5
+
+
+def _fp64_domain_samples(rng, n):
+    """Doubles across sqrt_rn's and rcp_rn's domains (rt_math.hpp): log-uniform exponents,
+    both signs for the reciprocal, the domain edges, all-ones and power-of-two significands,
+    1 - k 2^-53, multiples of 2^-32 and sums of squares of fp32 values (unit()'s arguments)."""
+    e = rng.uniform(-767.0, 1021.0, n)
+    m = rng.uniform(1.0, 2.0, n)
+    x = np.ldexp(m, np.floor(e).astype(np.int64))
+    edges = [2.0 ** -767, np.nextafter(2.0 ** -767, 1.0), 2.0 ** 1021, np.nextafter(2.0 ** 1022, 0.0), 1.0,
+             np.nextafter(1.0, 0.0), np.nextafter(1.0, 2.0), np.nextafter(2.0, 0.0), 3.0, 0.1, 2.0 ** -149]
+    pow2 = np.ldexp(1.0, np.arange(-767, 1022))
+    ones = np.ldexp(np.nextafter(2.0, 0.0), np.arange(-767, 1021))
+    near1 = 1.0 - np.arange(1, 4097) * 2.0 ** -53
+    u32 = rng.integers(1, 2 ** 32, n // 4).astype(np.float64) * 2.0 ** -32
+    f = rng.standard_normal((n // 4, 3)).astype(np.float32) * np.float32(2.0) ** rng.integers(-60, 60, (n // 4, 1))
+    f = f.astype(np.float32)
+    sq = (f.astype(np.float64) ** 2).sum(axis=1)
+    return np.concatenate([x, edges, pow2, ones, near1, u32, 1.0 - u32, sq[sq > 0]])
+
+
+@pytest.mark.gpu
+def test_device_sqrt_and_reciprocal_shortcuts_are_bit_exact(rt, gpu):
+    """rt_math.hpp sqrt_rn / rcp_rn (the unit-vector and Vec3.divide paths) equal the general
+    device expansions - and IEEE's correctly rounded results - bit for bit on their domains."""
+    from raytracer_amd import _lib
+    rng = np.random.default_rng(7)
+    x = _fp64_domain_samples(rng, 1 << 21)
+    xs = np.ascontiguousarray(np.concatenate([x, [0.0, -0.0, np.inf]]))
+    out = np.zeros((xs.size, 4), np.float64)
+    _lib.check(_lib.load().rt_debug_fp64(xs.size, xs.ctypes.data, out.ctypes.data))
+    bits = out.view(np.uint64)
+    assert np.array_equal(bits[:, 0], bits[:, 1]), int((bits[:, 0] != bits[:, 1]).sum())
+    assert np.array_equal(out[:, 1], np.sqrt(xs))
+    y = np.concatenate([x, -x])
+    y = y[(np.abs(y) >= 2.0 ** -767) & (np.abs(y) < 2.0 ** 1022)]
+    y = np.ascontiguousarray(y)
+    out = np.zeros((y.size, 4), np.float64)
+    _lib.check(_lib.load().rt_debug_fp64(y.size, y.ctypes.data, out.ctypes.data))
+    bits = out.view(np.uint64)
+    assert np.array_equal(bits[:, 2], bits[:, 3]), int((bits[:, 2] != bits[:, 3]).sum())
+    with np.errstate(over="ignore", under="ignore"):
+        assert np.array_equal(out[:, 3], 1.0 / y)
