@@ -222,12 +222,14 @@ __device__ __forceinline__ float pow5(float x) {
 }
 __device__ __forceinline__ double m_abs(double x) { return ::fabs(x); }
 __device__ __forceinline__ float m_abs(float x) { return ::fabsf(x); }
-__device__ __forceinline__ double m_sqrt(double x) { return ::sqrt(x); }
+// Math.sqrt: rt_math.hpp sqrt_rn wherever no range scaling applies (x >= 2^-767 or +inf / NaN: a
+// high word >= 0x10000000 as a signed integer, one compare), else the general expansion - the same
+// bits for every x.
+__device__ __forceinline__ double m_sqrt(double x) {
+    if (RT_FP64_SHORT && (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32) >= 0x10000000) return sqrt_rn(x);
+    return ::sqrt(x);
+}
 __device__ __forceinline__ float m_sqrt(float x) { return ::sqrtf(x); }
-// The square root of an argument known to be 0 or >= 2^-767 (rt_math.hpp sqrt_rn's domain):
-// a uniform draw r or 1 - r (multiples of 2^-32 below 1), or |1 - x| for a double x.
-__device__ __forceinline__ double m_sqrt_nz(double x) { return RT_FP64_SHORT ? sqrt_rn(x) : ::sqrt(x); }
-__device__ __forceinline__ float m_sqrt_nz(float x) { return ::sqrtf(x); }
 
 template <class Real> struct K {
     static constexpr Real PI = (Real)3.141592653589793;
@@ -1562,7 +1564,7 @@ __device__ __forceinline__ V3 dielectric_dir(Real ior, bool front, V3 din, V3 n,
     if (refl) return reflect<Real>(ud, n);
     // Vec3.refract (src/geometry/vec3.ts:193-209)
     const V3 perp = scale<Real>(add(ud, scale<Real>(n, cosT)), ratio);
-    const V3 par = scale<Real>(n, -m_sqrt_nz(m_abs((Real)1 - len2<Real>(perp))));
+    const V3 par = scale<Real>(n, -m_sqrt(m_abs((Real)1 - len2<Real>(perp))));
     return add(perp, par);
 }
 
@@ -1975,10 +1977,10 @@ __device__ __forceinline__ bool shade_diffuse(const DevScene& S, const RtCamera&
         const Real r1 = uniform<Real>(P.rng);
         const Real r2 = uniform<Real>(P.rng);
         const Real phi = (Real)2 * K<Real>::PI * r1;
-        const Real sr2 = m_sqrt_nz(r2);
+        const Real sr2 = m_sqrt(r2);
         Real sn, cs;
         m_sincos(phi, sn, cs);
-        gdir = onb_local<Real>(b, mk<Real>(cs * sr2, sn * sr2, m_sqrt_nz((Real)1 - r2)));
+        gdir = onb_local<Real>(b, mk<Real>(cs * sr2, sn * sr2, m_sqrt((Real)1 - r2)));
     } else {
         int pick = C.n_lights - 1;
         for (int l = 0; l < C.n_lights; ++l) {
