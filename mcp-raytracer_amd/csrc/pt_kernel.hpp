@@ -226,7 +226,7 @@ __device__ __forceinline__ float m_abs(float x) { return ::fabsf(x); }
 // high word >= 0x10000000 as a signed integer, one compare), else the general expansion - the same
 // bits for every x.
 __device__ __forceinline__ double m_sqrt(double x) {
-    if (RT_FP64_SHORT && (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32) >= 0x10000000) return sqrt_rn(x);
+    if ((RT_FP64_SHORT & 2) && (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32) >= 0x10000000) return sqrt_rn(x);
     return ::sqrt(x);
 }
 __device__ __forceinline__ float m_sqrt(float x) { return ::sqrtf(x); }
