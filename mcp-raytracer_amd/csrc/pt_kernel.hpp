@@ -1440,14 +1440,26 @@ struct NoHook {
     __device__ void operator()() const {}
 };
 // `after_prefilter`: called once the pre-filter pass is done (diagnostic section timer).
+#ifndef RT_PRE_AHEAD
+#define RT_PRE_AHEAD 1
+#endif
 template <class Real, bool COUNT, class Hook = NoHook>
 __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
                                                     uint16_t* lot, uint32_t* cnt, Hook after_prefilter = Hook()) {
     const FRay f = make_fray(r.o, r.d);
     const QuadPreRay qr = quad_pre_ray(f);
     uint32_t mask = 0u;
+    // one scalar load per record (wave-uniform), issued an iteration ahead: the scalar cache's
+    // latency was paid in full per primitive (s_waitcnt right after each load)
+    RtPre qn = ld_uniform(S.gpre, 0);
     for (int k = 0; k < n_prims; ++k) {
-        const RtPre q = ld_uniform(S.gpre, k);  // one scalar load (wave-uniform)
+        RtPre q;
+        if (RT_PRE_AHEAD) {
+            q = qn;
+            if (k + 1 < n_prims) qn = ld_uniform(S.gpre, k + 1);
+        } else {
+            q = ld_uniform(S.gpre, k);
+        }
         float lo;
         bool maybe;
         if (q.kind == PRE_SPHERE) {

@@ -3,6 +3,8 @@
 // the reference's JS doubles do.
 #include "launch.hpp"
 
+#include <cstdlib>
+
 namespace rt {
 
 hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const RtRegion& reg, const RenderOut& out,
@@ -221,8 +223,12 @@ hipError_t launch_adapt(const DevScene& S, const RtRegion& reg, const RenderOut&
 
 hipError_t launch_accum(const DevScene& S, const RtRegion& reg, const RenderOut& out, int tiles_x,
                         const SampleBuf& sb, hipStream_t stream) {
-    // about two blocks' worth of slots per thread-slot of the chip: 2 x 256 CUs x 1024 threads
-    const int grid = std::max(1, std::min((sb.slots + kAccBlock - 1) / kAccBlock, 2 * 256 * 1024 / kAccBlock));
+    // at most 1024 blocks (4 per CU), grid-stride beyond: the accumulate pass streams the records
+    // at ~5.6 TB/s either way; 1024 measured 2-3 % faster than 2048 or 4096 (Cornell 0.47 ->
+    // 0.455 ms, rain 3.19 -> 3.10 ms; profiles/r04/acc/). RT_AMD_ACC_BLOCKS overrides (A/B).
+    const char* e = std::getenv("RT_AMD_ACC_BLOCKS");
+    const int cap = e ? std::max(1, std::atoi(e)) : 1024;
+    const int grid = std::max(1, std::min((sb.slots + kAccBlock - 1) / kAccBlock, cap));
     hipLaunchKernelGGL(pt_accum_kernel, dim3(grid), dim3(kAccBlock), 0, stream, S, reg, out, tiles_x, sb);
     return hipGetLastError();
 }
