@@ -1440,26 +1440,17 @@ struct NoHook {
     __device__ void operator()() const {}
 };
 // `after_prefilter`: called once the pre-filter pass is done (diagnostic section timer).
-#ifndef RT_PRE_AHEAD
-#define RT_PRE_AHEAD 1
-#endif
 template <class Real, bool COUNT, class Hook = NoHook>
 __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
                                                     uint16_t* lot, uint32_t* cnt, Hook after_prefilter = Hook()) {
     const FRay f = make_fray(r.o, r.d);
     const QuadPreRay qr = quad_pre_ray(f);
     uint32_t mask = 0u;
-    // one scalar load per record (wave-uniform), issued an iteration ahead: the scalar cache's
-    // latency was paid in full per primitive (s_waitcnt right after each load)
-    RtPre qn = ld_uniform(S.gpre, 0);
     for (int k = 0; k < n_prims; ++k) {
-        RtPre q;
-        if (RT_PRE_AHEAD) {
-            q = qn;
-            if (k + 1 < n_prims) qn = ld_uniform(S.gpre, k + 1);
-        } else {
-            q = ld_uniform(S.gpre, k);
-        }
+        // one scalar load (wave-uniform). (Round 4 tried issuing the next record's load an
+        // iteration ahead: the two records' SGPRs pushed the pool kernel into SGPR spills,
+        // Cornell path kernel 13.93 -> 14.65 ms; profiles/r04/ahead/.)
+        const RtPre q = ld_uniform(S.gpre, k);
         float lo;
         bool maybe;
         if (q.kind == PRE_SPHERE) {
@@ -2348,6 +2339,12 @@ struct SampleBuf {
     // reference never renders (src/camera.ts:400-425). Bounce counts stay below 2^30
     // (loop_threshold caps depth at 1e9).
     int32_t err_in_rec;
+    // 12-byte records {r, g, b} (float triples at (float*)rec + 3 * index), the bounce statistics
+    // reduced by the path kernel itself (LaneBounces): fixed spp in colour mode without the
+    // per-pixel bounce output, where the accumulate pass needs only each pixel's colour sum in
+    // sample order - RenderStats' bounce total / min / max are order-free integer reductions
+    // (src/render-utils/renderStats.ts:21-35). A quarter less record traffic.
+    int32_t rec12;
     int32_t s0[kMaxPhases], chunk[kMaxPhases], nch[kMaxPhases], item_base[kMaxPhases];
     double rnch[kMaxPhases];  // 1.0 / nch
 };
@@ -2384,6 +2381,37 @@ __device__ __forceinline__ int rec_err_bits(int err_in_rec, unsigned long long& 
     return b;
 }
 
+template <bool NT>
+__device__ __forceinline__ void rec_store(float4* p, float4 r);
+typedef float RecF3 __attribute__((ext_vector_type(3), aligned(4)));  // a 12-byte record
+// A lane's bounce statistics over the samples it recorded (SampleBuf::rec12)
+struct LaneBounces {
+    uint32_t sum = 0, mn = 0xffffffffu, mx = 0;
+    __device__ void add(int b) {
+        sum += (uint32_t)b;
+        mn = min(mn, (uint32_t)b);
+        mx = max(mx, (uint32_t)b);
+    }
+    // into the launch's RenderStats (publish_stats): the accumulate pass adds none
+    __device__ void to(PixStats& st) const {
+        st.b = sum;
+        st.bmin = mn == 0xffffffffu ? ~0ull : (unsigned long long)mn;
+        st.bmax = mx;
+    }
+};
+// The sample's record at index `idx` (s * stride_s + slot * stride_slot): {rgb, w} or, with
+// rec12, {rgb} and w's bounce count into the lane's statistics.
+template <bool NT>
+__device__ __forceinline__ void rec_put(const SampleBuf& sb, size_t idx, V3 c, int w, LaneBounces& lb) {
+    if (sb.rec12) {
+        RecF3* p = reinterpret_cast<RecF3*>(reinterpret_cast<float*>(sb.rec) + 3 * idx);
+        if constexpr (NT) __builtin_nontemporal_store(RecF3{c.x, c.y, c.z}, p);
+        else *p = RecF3{c.x, c.y, c.z};
+        lb.add(w);
+    } else {
+        rec_store<NT>(sb.rec + idx, make_float4(c.x, c.y, c.z, __int_as_float(w)));
+    }
+}
 template <bool NT>
 __device__ __forceinline__ void rec_store(float4* p, float4 r) {
     if constexpr (NT) {
@@ -2560,6 +2588,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     constexpr bool RS = RT_RESUME && trav_fast(TRAV) && INSTR != 1;  // (INSTR 2: timed sections)
     FastWalk<Real> W;
     bool walking = false;
+    LaneBounces lb;  // SampleBuf::rec12
 
 #if RT_CHUNK_KOPQ
 #define PK_SB (kern_args().sb)
@@ -2606,12 +2635,8 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
         if constexpr (RS) {
             // the sample's radiance and bounce count to its record; next sample or idle
             auto finish_sample = [&](V3 c) {
-                float4 r;
-                r.x = c.x;
-                r.y = c.y;
-                r.z = c.z;
-                r.w = __int_as_float(P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err));
-                rec_store<false>(PK_SB.rec + ((size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot), r);
+                rec_put<false>(PK_SB, (size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot, c,
+                               P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err), lb);
                 ++s;
                 if (s < s_end) new_path = true;
                 else slot = -1;
@@ -2656,13 +2681,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
             V3 c;
             if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(PK_S, C, P, stk, stkt, cnt, st_err, pf, c)) {
-                float4 r;
-                r.x = c.x;
-                r.y = c.y;
-                r.z = c.z;
-                r.w = __int_as_float(P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err));
 #ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
-                rec_store<false>(PK_SB.rec + ((size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot), r);
+                rec_put<false>(PK_SB, (size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot, c,
+                               P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err), lb);
 #endif
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;
@@ -2676,6 +2697,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
         }
     }
     PixStats st;
+    lb.to(st);
     publish_stats(out, st, st_err, lane);
     publish_counters<COUNT, PROF>(out, cnt, pf, lane);
 #undef PK_SB
@@ -2819,14 +2841,11 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     // the sample's radiance and bounce count to its record; the slot's next phase
     // `err`: the sample's error flags (its miss without a background): in the record in
     // adaptive rounds (SampleBuf::err_in_rec), else in the launch's stats
+    LaneBounces lb;  // SampleBuf::rec12
     auto record = [&](V3 c, int bounces, int slot, int& s, int s_end, unsigned long long err = 0ull) -> int {
-        float4 r;
-        r.x = c.x;
-        r.y = c.y;
-        r.z = c.z;
-        r.w = __int_as_float(bounces | (sb.err_in_rec ? (int)((uint32_t)err << kRecErrShift) : 0));
         if (!sb.err_in_rec) st_err |= err;
-        rec_store<RT_REC_NT>(sb.rec + ((size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot), r);
+        rec_put<RT_REC_NT>(sb, (size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot, c,
+                           bounces | (sb.err_in_rec ? (int)((uint32_t)err << kRecErrShift) : 0), lb);
         ++s;
         return s < s_end ? PH_NEW : PH_ITEM;
     };
@@ -3035,6 +3054,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
         }
     }
     PixStats st;
+    lb.to(st);
     publish_stats(out, st, st_err, lane);
     publish_counters<false, PP>(out, cnt, pf, lane);
 }

@@ -42,9 +42,25 @@ __global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegi
             const int n = C.n_samples;
             // RT_ACC_UNROLL loads in flight; sample-major records are coalesced across the
             // wave, slot-major ones are one contiguous run per lane
-            const float4* rec = sb.rec + (size_t)slot * sb.stride_slot;
             const size_t stride = (size_t)sb.stride_s;
             int k = 0;
+            if (sb.rec12) {  // {r, g, b} records: the path kernel reduced the bounce statistics
+                             // (bsum 0, bmin / bmax at their neutral values here)
+                const RecF3* rec3 = reinterpret_cast<const RecF3*>(reinterpret_cast<const float*>(sb.rec) +
+                                                                   3 * (size_t)slot * sb.stride_slot);
+                for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
+                    RecF3 r[RT_ACC_UNROLL];
+#pragma unroll
+                    for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = rec3[(size_t)(k + m) * stride];
+#pragma unroll
+                    for (int m = 0; m < RT_ACC_UNROLL; ++m) color = add(color, v3(r[m].x, r[m].y, r[m].z));
+                }
+                for (; k < n; ++k) {
+                    const RecF3 r = rec3[(size_t)k * stride];
+                    color = add(color, v3(r.x, r.y, r.z));
+                }
+            }
+            const float4* rec = sb.rec + (size_t)slot * sb.stride_slot;
             for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
                 float4 r[RT_ACC_UNROLL];
 #pragma unroll

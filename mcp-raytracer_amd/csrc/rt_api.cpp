@@ -529,7 +529,9 @@ struct rt_camera {
             launch_adaptive_rounds(S, reg, out, g, mine, sb, schedule, run_pass, pass, stream);
         } else {
             // fixed spp: passes over at most sbuf_budget bytes of per-sample records
-            const size_t rec_per_tile = (size_t)kWave * (size_t)C.n_samples * sizeof(float4);
+            // 12-byte records where no pixel's bounce count is an output (SampleBuf::rec12)
+            sb.rec12 = C.mode != MODE_BOUNCES && !out.px_bounces && env_flag("RT_AMD_REC12", true);
+            const size_t rec_per_tile = (size_t)kWave * (size_t)C.n_samples * (sb.rec12 ? 12 : sizeof(float4));
             const long pass_tiles = std::max<long>(1, std::min<long>(mine, (long)(sbuf_budget() / rec_per_tile)));
             ensure_sbuf((size_t)pass_tiles * rec_per_tile);
             sb.rec = d_sbuf;
