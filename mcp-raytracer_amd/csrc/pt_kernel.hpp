@@ -2383,7 +2383,9 @@ __device__ __forceinline__ int rec_err_bits(int err_in_rec, unsigned long long& 
 
 template <bool NT>
 __device__ __forceinline__ void rec_store(float4* p, float4 r);
-typedef float RecF3 __attribute__((ext_vector_type(3), aligned(4)));  // a 12-byte record
+// a 12-byte record (loads / stores of a 3-element vector move 12 bytes; its sizeof is 16, so
+// records are addressed in floats)
+typedef float RecF3 __attribute__((ext_vector_type(3), aligned(4)));
 // A lane's bounce statistics over the samples it recorded (SampleBuf::rec12)
 struct LaneBounces {
     uint32_t sum = 0, mn = 0xffffffffu, mx = 0;

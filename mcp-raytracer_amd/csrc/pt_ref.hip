@@ -46,17 +46,18 @@ __global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegi
             int k = 0;
             if (sb.rec12) {  // {r, g, b} records: the path kernel reduced the bounce statistics
                              // (bsum 0, bmin / bmax at their neutral values here)
-                const RecF3* rec3 = reinterpret_cast<const RecF3*>(reinterpret_cast<const float*>(sb.rec) +
-                                                                   3 * (size_t)slot * sb.stride_slot);
+                // (addresses in floats: a 3-element vector type's size is 16 bytes, its loads 12)
+                const float* rec3 = reinterpret_cast<const float*>(sb.rec) + 3 * (size_t)slot * sb.stride_slot;
+                const size_t step = 3 * stride;
                 for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
                     RecF3 r[RT_ACC_UNROLL];
 #pragma unroll
-                    for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = rec3[(size_t)(k + m) * stride];
+                    for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = *reinterpret_cast<const RecF3*>(rec3 + (size_t)(k + m) * step);
 #pragma unroll
                     for (int m = 0; m < RT_ACC_UNROLL; ++m) color = add(color, v3(r[m].x, r[m].y, r[m].z));
                 }
                 for (; k < n; ++k) {
-                    const RecF3 r = rec3[(size_t)k * stride];
+                    const RecF3 r = *reinterpret_cast<const RecF3*>(rec3 + (size_t)k * step);
                     color = add(color, v3(r.x, r.y, r.z));
                 }
             }
