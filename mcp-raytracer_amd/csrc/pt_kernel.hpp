@@ -2116,6 +2116,9 @@ __device__ __forceinline__ void stats_atomics(const RenderOut& out, unsigned lon
         atomicAdd(&w[ST_SAMPLES * kStatStride], ss);
         atomicMin(&w[ST_SMIN * kStatStride], smn);
         atomicMax(&w[ST_SMAX * kStatStride], smx);
+    }
+    // bounce words also from the path kernels' lanes (12-byte records: LaneBounces, no pixels)
+    if (sp > 0 || bmn != ~0ull) {
         atomicAdd(&w[ST_BOUNCES * kStatStride], sb);
         atomicMin(&w[ST_BMIN * kStatStride], bmn);
         atomicMax(&w[ST_BMAX * kStatStride], bmx);
