@@ -793,13 +793,17 @@ def test_multipass_chunked_equals_single_pass(rt, gpu, monkeypatch):
     monkeypatch.setenv("RT_AMD_CHUNKED", "1")
     cam1, rgb1, rad1, st1 = _render_gpu(rt, sd, ro)
     assert cam1.pass_count() == 1
-    monkeypatch.setenv("RT_AMD_SBUF_MB", "1")  # 1 MB / (64 px x 37 x 16 B) = 27 tiles per pass: 6 passes
-    cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
-    assert cam2.pass_count() == 6
-    path_ms, acc_ms = cam2.kernel_times()
-    assert path_ms > 0 and acc_ms > 0
-    assert np.array_equal(rgb1, rgb2) and np.array_equal(rad1, rad2, equal_nan=True)
-    assert st1.samples == st2.samples and st1.bounces == st2.bounces
+    # 1 MB / (64 px x 37 x 12 B) = 36 tiles per pass: 4 passes of the 144 tiles; with 16-byte
+    # records (RT_AMD_REC12=0: the bounce word in the record) 27 tiles per pass: 6 passes
+    monkeypatch.setenv("RT_AMD_SBUF_MB", "1")
+    for rec12, passes in (("1", 4), ("0", 6)):
+        monkeypatch.setenv("RT_AMD_REC12", rec12)
+        cam2, rgb2, rad2, st2 = _render_gpu(rt, sd, ro)
+        assert cam2.pass_count() == passes
+        path_ms, acc_ms = cam2.kernel_times()
+        assert path_ms > 0 and acc_ms > 0
+        assert np.array_equal(rgb1, rgb2) and np.array_equal(rad1, rad2, equal_nan=True)
+        assert st1.samples == st2.samples and st1.bounces == st2.bounces
 
 
 def test_release_device_then_render_again(rt, gpu):
