@@ -806,6 +806,31 @@ def test_multipass_chunked_equals_single_pass(rt, gpu, monkeypatch):
         assert st1.samples == st2.samples and st1.bounces == st2.bounces
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,kernel_env", [("cornell", {}), ("spheres", {}), ("cornell", {"RT_AMD_CHUNKED": "1"})])
+def test_twelve_byte_records_equal_sixteen_byte_records(rt, gpu, monkeypatch, scene, kernel_env):
+    """SampleBuf::rec12: {r, g, b} records with the bounce statistics reduced per lane in the
+    path kernel give the 16-byte records' image and RenderStats (bounce total / min / max
+    included) on the pool and the chunked kernel, over a region that cuts tiles."""
+    opts = {"cornell": {"type": "cornell"}, "spheres": {"type": "spheres", "options": {"count": 200, "seed": 3}}}[scene]
+    sd = rt.generate_scene_data(opts)
+    ro = {"width": 72, "samples": 21, "depth": 12, **NOADAPT}
+    for k, v in kernel_env.items():
+        monkeypatch.setenv(k, v)
+    out = []
+    for rec12 in ("1", "0"):
+        monkeypatch.setenv("RT_AMD_REC12", rec12)
+        cam = rt.create_camera_from_scene_data(sd, ro)
+        W, H = cam.image_width, cam.image_height
+        rgb = np.zeros((H, W, 3), np.uint8)
+        rad = np.zeros((H, W, 3), np.float32)
+        st = cam.render_region(rgb, (3, 5, W - 7, H - 9), radiance=rad)
+        out.append((rgb, rad, st))
+    (a_rgb, a_rad, a_st), (b_rgb, b_rad, b_st) = out
+    assert_identical(a_rad, a_rgb, b_rad, b_rgb, f"rec12 vs rec16 {scene} {kernel_env}")
+    assert a_st.pixels == b_st.pixels and a_st.samples == b_st.samples and a_st.bounces == b_st.bounces
+
+
 def test_release_device_then_render_again(rt, gpu):
     """rt_camera_release_device frees every device buffer and nulls it; the next
     render must re-create all of them (no use of a freed frame buffer)."""
