@@ -165,6 +165,8 @@ def parse_args(argv):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--repeats", type=int, default=3,
+                    help="timed repeats of --steps steps; the median repeat is reported (SURVEY.md §8d)")
     ap.add_argument("--scene", default="cornell", choices=sorted(SCENES))
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--spp", type=int, default=256)
@@ -336,18 +338,22 @@ def main(argv=None):
         step()
         torch.cuda.synchronize()
         log(f"warmup {i + 1}/{args.warmup}")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step()
-        if args.steps <= 5 or (i + 1) % 10 == 0:  # no sync here: keep launches queued
-            log(f"step {i + 1}/{args.steps} queued")
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    # three repeats, the median reported. Each repeat times exactly `steps`
+    # steps between a barrier + synchronize on both sides; the max over ranks is taken per repeat.
+    reps = []
+    for r in range(args.repeats):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step()
+            if args.steps <= 5 or (i + 1) % 10 == 0:  # no sync here: keep launches queued
+                log(f"repeat {r + 1}/{args.repeats}: step {i + 1}/{args.steps} queued")
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        reps.append(time.perf_counter() - t0)
 
     # Kernel time of the dominant kernel, from HIP events the library records on
     # the launch stream (per pass, path kernel and accumulate separately), over
@@ -364,10 +370,11 @@ def main(argv=None):
     kind = cam.last_kernel()  # the path kernel the library launched (rt_camera_last_kernel)
     kernel_name = {"pool": "pt_pool_kernel", "chunked": "pt_chunk_kernel"}.get(kind, "pt_render_kernel")
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    t = torch.tensor([*reps, kernel_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t[0])
+    reps = [float(x) for x in t[:len(reps)]]
+    elapsed = sorted(reps)[len(reps) // 2]  # the median repeat (max over ranks)
 
     # Untimed: the same frame again with its fp32 radiance (assembled over the ranks
     # like the timed frames) and the merged RenderStats, for the checks below.
@@ -412,6 +419,8 @@ def main(argv=None):
             "metric": metric_for(args.scene, W, H, args.spp, args.depth, args.adaptive), "value": round(value, 3),
             "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "repeats": {"n": len(reps), "reported": "median",
+                        "ms_per_step": [round(x / args.steps * 1e3, 3) for x in reps]},
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64" if args.precision == "ref" else "f32",
             "data": "synthetic: reference scene generator output (deterministic), path RNG seed "

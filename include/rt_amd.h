@@ -173,6 +173,14 @@ int rt_debug_math(int32_t n, const uint32_t* u, double* out);
  * 1 / x} (pins rt_math.hpp sqrt_rn / rcp_rn bit for bit on their domains). */
 int rt_debug_fp64(int32_t n, const double* x, double* out);
 
+/* Pass sizing of a fixed-spp / adaptive launch (host only, no device): the units (64-slot
+ * tile groups) one pass of the path kernel takes out of `units`, given each unit's slots,
+ * the guided schedule's chunks per slot (items per slot), each unit's record bytes and the
+ * record budget. A pass never numbers 2^31 - 2^22 or more items (the hand-out counter's
+ * headroom): a budget past that gives more passes, not an error. */
+int rt_debug_pass_plan(int64_t units, int64_t unit_slots, int64_t chunks_per_slot, int64_t rec_bytes_per_unit,
+                       int64_t budget_bytes, int64_t* pass_units);
+
 /* The path RNG stream (seeded Math.random replacement), host evaluation. */
 int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out);
 

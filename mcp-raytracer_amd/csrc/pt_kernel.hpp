@@ -98,6 +98,7 @@ constexpr uint32_t kRecBounceMask = (1u << kRecErrShift) - 1u;
 enum {
     PR_NEWPATH = 0, PR_RR, PR_HIT, PR_MISS, PR_HITREC, PR_SCATTER, PR_SAMPLE, PR_PDF, PR_ACC, PR_TILE,
     PR_NODE, PR_LEAF,  // lane counts only (no cycles): node-step and leaf-test iterations of the walk
+    PR_WNODE, PR_WLEAF,  // resumable walk: cycles of its node-step loops / leaf phases (part of PR_HIT's walk)
     PR_LOOP, PR_TRIPS, PR_WORDS
 };
 // INSTR == 2 also records, per section k < PR_LOOP, the lanes active when a wave
@@ -613,14 +614,25 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
     FRay f;
     f.o[0] = o.x; f.o[1] = o.y; f.o[2] = o.z;
     f.d[0] = d.x; f.d[1] = d.y; f.d[2] = d.z;
-    float m = 0.0f;
+    float m = 0.0f, mall = 0.0f;
+    const float dmax = ::fmaxf(::fmaxf(::fabsf(d.x), ::fabsf(d.y)), ::fabsf(d.z));
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float c = f.d[a];
         const float cc = ::fabsf(c) < 1e-30f ? ::copysignf(1e-30f, c) : c;
         f.inv[a] = __builtin_amdgcn_rcpf(cc);  // <= 1 ulp: a common factor of an axis' two planes
         f.noi[a] = -(f.o[a] * f.inv[a]);
-        m = ::fmaxf(m, ::fabsf(f.noi[a]));
+        const float an = ::fabsf(f.noi[a]);
+        mall = ::fmaxf(mall, an);
+        // near-parallel axes (|d_a| < 1e-3 max|d|) stay out of eps (an exact zero
+        // component, inv = 1e30, made eps ~1e24 and every box accepted). Their planes need no
+        // absolute slack: the fused error is u|o_a inv_a| + relative terms, and for a face b
+        // either |o_a| <= 4 (1 + |b|), where the box's outward padding of 1e-6 (1 + |b|)
+        // (scene.cpp make_fast_nodes) is >= 2u|o_a| in coordinates, so the padded face's computed
+        // t stays outside the unpadded face's exact t; or |o_a| > 4 (1 + |b|), where
+        // |t_a| = |b - o_a| |inv_a| >= 0.75 |o_a inv_a| and the error is relative, <= 2.7u |t_a|,
+        // inside slab_accept's relative 2e-6 (~33u) with the rcp and fma roundings (~3u).
+        m = ::fabsf(c) >= 1e-3f * dmax ? ::fmaxf(m, an) : m;
         f.nrow[a] = 16 * a + (RT_NEARFAR && f.inv[a] < 0.0f ? 48 : 0);
     }
     // 1e-6 * max|o * inv| ~ 16 u: covers the rounding of o * inv at both ends of the interval
@@ -629,7 +641,7 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
     f.ia = __builtin_amdgcn_rcpf(f.a);
     f.dn = __builtin_amdgcn_sqrtf(f.a) * (1.0f + kRel);
     f.pthr = 1e-3f * f.dn;
-    if (!(m < 1e37f)) {  // o * inv overflowed (|o| > ~1e7 with an axis-parallel d): cull nothing
+    if (!(mall < 1e37f)) {  // o * inv overflowed (|o| > ~1e7 with an axis-parallel d): cull nothing
 #pragma unroll
         for (int a = 0; a < 3; ++a) f.inv[a] = f.noi[a] = 0.0f;
         f.eps = __builtin_inff();
@@ -1200,6 +1212,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 }
                 if (__ballot(leaf == kTravDone) == 0ull) break;  // every walking lane holds a leaf
             }
+            if (PROF) psec<PROF>(*pf, PR_WNODE);
             if (leaf == kTravDone && ref != kTravDone) {
                 leaf = ref;
                 ref = pop();
@@ -1216,6 +1229,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                     ref = pop();
                 }
             }
+            if (PROF) psec<PROF>(*pf, PR_WLEAF);
             W.ref = ref;
             W.leaf = leaf;
             W.sp = sp;
@@ -2390,10 +2404,13 @@ __device__ __forceinline__ void rec_store(float4* p, float4 r);
 // records are addressed in floats)
 typedef float RecF3 __attribute__((ext_vector_type(3), aligned(4)));
 // A lane's bounce statistics over the samples it recorded (SampleBuf::rec12)
+// (sum in 64 bits: a lane records ~10^4 samples per launch at the 8 GB record budget and depth
+// goes up to 1e9, so a 32-bit sum could wrap - ADVICE r04)
 struct LaneBounces {
-    uint32_t sum = 0, mn = 0xffffffffu, mx = 0;
+    unsigned long long sum = 0;
+    uint32_t mn = 0xffffffffu, mx = 0;
     __device__ void add(int b) {
-        sum += (uint32_t)b;
+        sum += (unsigned long long)(uint32_t)b;
         mn = min(mn, (uint32_t)b);
         mx = max(mx, (uint32_t)b);
     }

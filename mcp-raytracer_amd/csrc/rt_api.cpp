@@ -73,6 +73,20 @@ int device_cus(int dev) {
     return cus;
 }
 
+// Pass sizing of the chunked / pool kernels. A pass hands out its items through one int32
+// counter (take_pool), which may overshoot the item count by 2 x grid waves x pool before the
+// last wave sees it exhausted: items must stay below kItemCap. A pass of `units` groups of
+// `unit_slots` pixel slots numbers ceil64(units * unit_slots) x chunks_per_slot items
+// (chunks_per_slot = the schedule's sum of nch: one item per (slot, chunk)). So each pass is
+// the smallest of: the units left, the record budget, and the counter headroom - a larger
+// record budget gives fewer, bounded passes instead of an error.
+constexpr long kItemCap = (1l << 31) - (1l << 22);
+long pass_units(long units_left, long unit_slots, long chunks_per_slot, size_t rec_bytes_per_unit, size_t budget) {
+    const long by_budget = (long)(budget / std::max<size_t>(rec_bytes_per_unit, 1));
+    const long by_items = (kItemCap - 1) / (std::max<long>(unit_slots, 1) * std::max<long>(chunks_per_slot, 1));
+    return std::max<long>(1, std::min(units_left, std::min(by_budget, by_items)));
+}
+
 }  // namespace
 
 // error hook for the other translation units of the library (image.cpp)
@@ -510,7 +524,7 @@ struct rt_camera {
                 sb.item_base[p] = (int32_t)items;
                 items += group_slots * sb.nch[p];
             }
-            if (items >= (1l << 31) - (1l << 22)) throw std::runtime_error("chunked pass too large");  // counter headroom: 2 x grid waves x pool
+            if (items >= kItemCap) throw std::runtime_error("chunked pass too large");  // pass_units keeps it below
             sb.n_items = (int32_t)items;
             if (!first) hip_check(hipMemsetAsync(d_tile, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");
             LaunchGeom gp = g;
@@ -532,10 +546,10 @@ struct rt_camera {
             // 12-byte records where no pixel's bounce count is an output (SampleBuf::rec12)
             sb.rec12 = C.mode != MODE_BOUNCES && !out.px_bounces && env_flag("RT_AMD_REC12", true);
             const size_t rec_per_tile = (size_t)kWave * (size_t)C.n_samples * (sb.rec12 ? 12 : sizeof(float4));
-            const long pass_tiles = std::max<long>(1, std::min<long>(mine, (long)(sbuf_budget() / rec_per_tile)));
+            schedule((double)mine * kWave, C.n_samples);
+            const long pass_tiles = pass_units(mine, kWave, chunks_per_slot(sb), rec_per_tile, sbuf_budget());
             ensure_sbuf((size_t)pass_tiles * rec_per_tile);
             sb.rec = d_sbuf;
-            schedule((double)mine * kWave, C.n_samples);
             for (long t0 = 0; t0 < mine; t0 += pass_tiles, ++pass) {
                 const long nt = std::min(pass_tiles, mine - t0);
                 sb.tile0 = (int32_t)t0;
@@ -609,8 +623,9 @@ struct rt_camera {
             sb.err_in_rec = 1;
             schedule((double)n_act, len);
             const size_t rec_per_slot = (size_t)len * sizeof(float4);
-            const long pass_slots = std::max<long>(kWave, std::min<long>((n_act + kWave - 1) / kWave * kWave,
-                                                                        (long)(sbuf_budget() / rec_per_slot) / kWave * kWave));
+            // passes of whole 64-slot groups (items are numbered per group of 64 slots)
+            const long pass_slots =
+                kWave * pass_units((n_act + kWave - 1) / kWave, kWave, chunks_per_slot(sb), rec_per_slot * kWave, sbuf_budget());
             ensure_sbuf((size_t)pass_slots * rec_per_slot);
             sb.rec = d_sbuf;
             hip_check(hipMemsetAsync(d_acount, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
@@ -670,6 +685,11 @@ struct rt_camera {
         sbuf_cap = 0;
         hip_check(hipMalloc(&d_sbuf, bytes), "hipMalloc(sample buffer)");
         sbuf_cap = bytes;
+    }
+    static long chunks_per_slot(const SampleBuf& sb) {
+        long n = 0;
+        for (int p = 0; p < sb.n_phases; ++p) n += sb.nch[p];
+        return n;
     }
     static size_t sbuf_budget() {
         const char* e = std::getenv("RT_AMD_SBUF_MB");
@@ -1019,6 +1039,16 @@ int rt_debug_fp64(int32_t n, const double* x, double* out) {
         if (d_out) (void)hipFree(d_out);
         return set_error(RT_ERR_DEVICE, e.what());
     }
+}
+
+int rt_debug_pass_plan(int64_t units, int64_t unit_slots, int64_t chunks_per_slot, int64_t rec_bytes_per_unit,
+                       int64_t budget_bytes, int64_t* pass_units_out) {
+    if (units < 0 || unit_slots < 1 || chunks_per_slot < 1 || rec_bytes_per_unit < 1 || budget_bytes < 1 ||
+        !pass_units_out)
+        return set_error(RT_ERR_INVALID, "bad arguments");
+    *pass_units_out = pass_units((long)units, (long)unit_slots, (long)chunks_per_slot, (size_t)rec_bytes_per_unit,
+                                 (size_t)budget_bytes);
+    return RT_OK;
 }
 
 int rt_debug_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int32_t n, uint32_t* out) {

@@ -72,7 +72,8 @@ RT_HD V3 scale(V3 a, Real t) {
 //    2^1022 unscaled and sets no post-scale flag, the numerator's product 1 * r is exact,
 //    div_fmas is then a plain fma and div_fixup the identity on the finite non-zero quotient):
 //    v_rcp_f64, two Newton steps, one residual correction. Valid for 2^-767 <= |y| < 2^1022.
-// tests/test_gpu_parity.py checks both against ::sqrt and 1.0 / y on the device (rt_debug_math).
+// tests/test_v8_math.py::test_device_sqrt_and_reciprocal_shortcuts_are_bit_exact checks both
+// against ::sqrt and 1.0 / y on the device (rt_debug_fp64).
 __device__ __forceinline__ double sqrt_rn(double x) {
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y;

@@ -23,7 +23,7 @@ TRAVERSAL = {"fast": 0, "reference": 1, "brute": 2, "auto": 3}
 CT_NAMES = ["node", "sphere", "quad", "plane", "material", "light_quad", "light_sphere",
             "bounces", "diffuse", "samples", "rays", "exact", "exact_wave", "cand0", "cand2", "exact2"]
 PR_NAMES = ["newpath", "rr", "hit", "miss", "hitrec", "scatter", "sample", "pdf", "acc", "tile", "node", "leaf",
-            "loop", "trips"]
+            "wnode", "wleaf", "loop", "trips"]
 COUNTER_WORDS = 64
 STATS_WORDS = 8  # RT_STATS_WORDS: pixels, samples, smin, smax, bounces, bmin, bmax, error
 
@@ -84,6 +84,8 @@ _SIGS = {
     "rt_camera_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                    C.c_void_p]),
     "rt_debug_world_hit": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_debug_pass_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                     C.POINTER(C.c_int64)]),
     "rt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_void_p]),
     "rt_debug_math": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_debug_fp64": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),

@@ -214,6 +214,9 @@ def render_frame(camera, frame, rank: int, world: int, stream=None, precision=No
     g = gather_slabs(slab, world, out=gathered)
     gr = gather_slabs(rad_slab, world, out=rad_gathered) if radiance is not None else None
     if rank != 0:
+        # the gather still reads `slab` on torch's current stream: a next render queued on
+        # `stream` must not overwrite it first
+        _wait_for_current(stream, frame.device)
         return None
     cur = torch.cuda.current_stream(frame.device).cuda_stream
     unpack_tiles(g, region, W, H, frame, cur, slab_tiles=n_tiles + 1)

@@ -209,3 +209,39 @@ def test_device_png_encoder_filters_and_blocks(rt):
         assert ftypes <= {0, 1, 2, 3, 4}
         if name == "gradient":
             assert ftypes - {0}, "a gradient should pick a predicting filter"
+
+
+def test_pass_plan_caps_items_at_the_counter_headroom(rt):
+    """a record budget past the int32 hand-out counter's headroom gives more,
+    bounded passes instead of the 'chunked pass too large' error (rt_api.cpp pass_units).
+    Config 5 (4096^2, spp 1024: 262,144 tiles; a 1-sample-chunk schedule numbers up to 1,024
+    items per slot) at the 32 GB budget that failed in round 4 (profiles/r04/sbuf/)."""
+    from raytracer_amd import _lib
+    lib = _lib.load()
+    cap = (1 << 31) - (1 << 22)
+
+    def plan(units, slots, chunks, rec, budget):
+        out = ctypes.c_int64(0)
+        _lib.check(lib.rt_debug_pass_plan(units, slots, chunks, rec, budget, ctypes.byref(out)))
+        return out.value
+
+    tiles, spp = 4096 * 4096 // 64, 1024
+    rec_tile = 64 * spp * 12
+    for chunks in (spp, 600, 64):
+        for budget_mb in (8192, 32768, 1 << 20):
+            per = plan(tiles, 64, chunks, rec_tile, budget_mb << 20)
+            assert 1 <= per <= tiles
+            assert per * 64 * chunks < cap                      # every pass fits the counter
+            assert per <= max(1, (budget_mb << 20) // rec_tile)  # and the record budget
+            passes = -(-tiles // per)
+            assert passes * per >= tiles
+    # the budget that fit in round 4 still gives the same pass (8 GB: 10,922 tiles, 25 passes)
+    assert plan(tiles, 64, spp, rec_tile, 8192 << 20) == (8192 << 20) // rec_tile
+    # past the headroom the counter, not the budget, sizes the pass
+    big = plan(tiles, 64, spp, rec_tile, 32768 << 20)
+    assert big == (cap - 1) // (64 * spp) < (32768 << 20) // rec_tile
+    # a small launch takes one pass; a budget below one unit still makes progress
+    assert plan(10, 64, 16, 1000, 1 << 30) == 10
+    assert plan(10, 64, 16, 1 << 20, 1) == 1
+    with pytest.raises(_lib.RtError):
+        plan(10, 0, 16, 1000, 1 << 30)

@@ -222,3 +222,41 @@ def test_merge_stats_words_skips_empty_ranks_and_ors_errors():
     w[2, 7] = 2
     with pytest.raises(RuntimeError, match="emission stack"):
         stats_from_words(merge_stats_words(w).tolist())
+
+
+def test_render_frame_orders_the_render_stream_after_the_gather_on_every_rank(monkeypatch):
+    """on ranks above 0 the gather still reads `slab` on torch's current stream
+    when render_frame returns; the caller's render stream must be made to wait for it (so a
+    next render into a reused slab cannot overwrite it), as on rank 0. The device calls are
+    stood in for; what is checked is the order of the stream hand-offs."""
+    sys.path.insert(0, str(ROOT / "mcp-raytracer_amd"))
+    from raytracer_amd import distributed as D
+
+    calls = []
+
+    class Cam:
+        image_width, image_height = 16, 16
+
+        def render_device(self, **kw):
+            calls.append(("render", kw["stream"]))
+
+        def stats_words(self, ptr, stream):
+            calls.append(("stats", stream))
+
+    class Slab:
+        def numel(self):
+            return 10 ** 6
+
+        def data_ptr(self):
+            return 0
+
+    class Frame:
+        device = "cuda:0"
+
+    monkeypatch.setattr(D, "_wait", lambda s, d: calls.append(("wait", s)))
+    monkeypatch.setattr(D, "_wait_for_current", lambda s, d: calls.append(("wait_for_current", s)))
+    monkeypatch.setattr(D, "gather_slabs", lambda slab, world, out=None: calls.append(("gather",)) or None)
+    assert D.render_frame(Cam(), Frame(), rank=1, world=2, stream=1234, slab=Slab()) is None
+    names = [c[0] for c in calls]
+    assert names == ["render", "stats", "wait", "gather", "wait_for_current"]
+    assert calls[-1] == ("wait_for_current", 1234)

@@ -12,11 +12,14 @@
 #   prof              bench under rocprofv3 --kernel-trace --stats (csv)
 #   valu / traffic    the VALU / HBM counter passes of the bench configs + fp32 + adaptive (separate --pmc runs)
 #   valu5 / traffic5  the same for BASELINE config 5 (spheres-100k 4096^2 spp1024 depth 100, 32 passes)
-#   rankshare         tools/rank_share.py for Cornell and spheres-500
+#   rankshare         tools/rank_share.py: every tile group of N = 2, 4, 8 (max / min / mean) + RCCL gather + unpack
 #   sections          tools/profile_sections.py (section timers of the chunked / sequential kernels)
 #   poolsections      the same for the pool kernel (variant library 'poolprof': RT_POOL_PROF=1, RT_POOL_K=146)
 #   countexact        tools/count_exact.py (exact tests per ray / per wave-trip)
 #   bench:<args>      one extra bench line with <args> (underscores become spaces)
+#   ab                runtime-knob A/B (tools/ab_env.sh) over $CFGS x $ARMS (set by the caller:
+#                     lines "tag bench-args" / "arm ENV=V ..."), table in $O/ab/table.txt
+#   abvar             library-variant A/B: $ARMS lines "arm variant" (RT_AMD_VARIANT, '-' = default lib)
 # Every GPU step runs under its own time limit; the first failing step ends the script.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
@@ -55,10 +58,22 @@ for step in "$@"; do
     valu5) VALU_DIR=$O/valu5 bash tools/pmc_valu.sh "$CFG5" || exit $? ;;
     traffic) TRAFFIC_DIR=$O/traffic bash tools/pmc_traffic.sh "${CFGS4[@]}" "--precision fp32" "--adaptive" || exit $? ;;
     traffic5) TRAFFIC_DIR=$O/traffic5 bash tools/pmc_traffic.sh "$CFG5" || exit $? ;;
-    rankshare)
-      run 200 rank_share_cornell.log python tools/rank_share.py cornell || exit $?
-      run 200 rank_share_spheres.log python tools/rank_share.py spheres || exit $? ;;
+    rankshare) run 400 rank_share.log python tools/rank_share.py cornell spheres rain || exit $? ;;
     sections) run 300 sections.log python tools/profile_sections.py || exit $? ;;
+    sections:*) run 300 sections_${step#sections:}.log python tools/profile_sections.py ${step#sections:} || exit $? ;;
+    ab) OUT=$O/ab bash tools/ab_env.sh || exit $?; python tools/ab_table.py $O/ab > $O/ab/table.txt ;;
+    abvar)
+      mkdir -p $O/ab
+      echo "$CFGS" | while read -r tag args; do
+        [ -z "$tag" ] && continue
+        echo "$ARMS" | while read -r arm var; do
+          [ -z "$arm" ] && continue
+          if [ "$var" = "-" ]; then vv=""; else vv=$var; fi
+          RT_AMD_VARIANT=$vv run ${TLIM:-200} ab/${tag}_${arm}.log python bench.py --steps ${STEPS:-5} --warmup 1 \
+            --no-cpu --no-count --no-parity $args || exit $?
+        done || exit $?
+      done || exit $?
+      python tools/ab_table.py $O/ab > $O/ab/table.txt ;;
     poolsections) RT_AMD_VARIANT=poolprof run 300 sections_pool.log python tools/profile_sections.py cornell || exit $? ;;
     countexact) run 300 count_exact.log python tools/count_exact.py || exit $? ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
