@@ -23,8 +23,9 @@ struct LaunchGeom {
 
 // LDS budget (stack + [tnodes][prims]) up to which the scene is copied into LDS.
 constexpr int kLdsSceneMaxBytes = 152 * 1024;
-// Static LDS of the chunked / pool kernels (the phase table), beside the dynamic allocation.
-constexpr size_t kStaticLdsBytes = 512;
+// Static LDS of the chunked / pool kernels (the phase table; with RT_COOP_LEAF the per-wave
+// segment-start tables, 128 bytes per wave), beside the dynamic allocation.
+constexpr size_t kStaticLdsBytes = 512 + (RT_COOP_LEAF ? (size_t)(kBlockChunk / kWave) * kWave * 2 : 0);
 // ... plus the per-wave section timers of the diagnostic variants: every kernel of a
 // count == 2 launch, and every pool kernel of an RT_POOL_PROF build.
 inline size_t static_lds_bytes(int count, bool pool) {

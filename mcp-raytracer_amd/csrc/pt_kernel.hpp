@@ -107,6 +107,8 @@ enum {
 struct Prof;  // diagnostic section timer (below)
 template <bool PROF>
 __device__ __forceinline__ void pcount(Prof& pf, int k);
+template <bool PROF>
+__device__ __forceinline__ void psec(Prof& pf, int k);
 constexpr int kCounterWords = 64;  // CT_WORDS + PR_WORDS + 2 * PR_LOOP, rounded up
 static_assert(CT_WORDS + PR_WORDS + 2 * PR_LOOP <= kCounterWords, "counter words");
 
@@ -974,14 +976,35 @@ __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Re
     }
 }
 
-template <class Real, bool COUNT, bool DEFER>
+// RT_LEAF_PREFETCH: a leaf's compact records (tsph) and leaf slots (tprims) are loaded for up to
+// four primitives at once, before the first pre-filter, so a leaf costs one memory latency instead
+// of one per primitive (trees walked from global memory: every tsph / tprims read is an L2 round
+// trip). Entries past the leaf's end read the records that follow it - the next leaf's, or the
+// next blob section's (tprims is followed by tsph, tsph by prims) - and are never used.
+// 0: off, 1: trees walked from global memory (LDSS 0), 2: every fast-traversal launch.
+#ifndef RT_LEAF_PREFETCH
+#define RT_LEAF_PREFETCH 0
+#endif
+template <class Real, bool COUNT, bool DEFER, bool PF = false>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
                                           Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt) {
     const int v = ~ref;
     const int first = v >> 3;
     const int end = first + (v & 7);
+    float4 gq[PF ? 4 : 1];
+    int kq[PF ? 4 : 1];
     for (int m = first; m < end; ++m) {
-        const float4 g = S.tsph[m];
+        const int j = (m - first) & 3;
+        if constexpr (PF) {
+            if (j == 0) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    gq[u] = S.tsph[m + u];
+                    kq[u] = S.tprims[m + u];
+                }
+            }
+        }
+        const float4 g = PF ? gq[j] : S.tsph[m];
         Real t;
         int k;  // reference leaf slot (the tie-break key)
         bool cand;
@@ -991,7 +1014,7 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
             if constexpr (DEFER) {
             float hi;
             if (!sphere_maybe_hi(g, f, thi, lo, hi)) continue;
-            k = S.tprims[m];
+            k = PF ? kq[j] : S.tprims[m];
             // a second candidate: one surely hit before the pending one's lower bound
             // replaces it untested (t_new <= hi < plo <= t_pending); otherwise the
             // pending one is settled first
@@ -1005,11 +1028,11 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
             } else {
             if (!sphere_maybe(g, f, thi, lo)) continue;
             if (COUNT) count_exact(cnt);
-            k = S.tprims[m];
+            k = PF ? kq[j] : S.tprims[m];
             cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
             }
         } else {
-            k = S.tprims[m];
+            k = PF ? kq[j] : S.tprims[m];
             cand = prim_candidate<Real, COUNT>(S.prims[k], ray_at_use<Real>(r), f, thi, t, cnt);
         }
         if (cand && (t < best_t || (t == best_t && k < best))) {
@@ -1149,10 +1172,155 @@ __device__ __forceinline__ void fast_walk_begin(const DevScene& S, V3 o, V3 d, F
     W.ref = slab(S.root_box, f, W.thi, tn0) ? S.troot : kTravDone;
 }
 
+// ---------------------------------------------------------------------------
+// Cooperative leaf phase (RT_COOP_LEAF): the leaf tests of a round, flattened over the wave.
+// In the parked-leaf walk each lane tests its own leaf's 1-7 primitives in turn, so a leaf
+// phase issues the fp32 pre-filter max(count) times at the lanes that hold a leaf (spheres-500:
+// 20.5 of 64 lanes per leaf test, round-4 sections.log). Here every (lane, primitive) pair of
+// the wave's parked leaves gets its own lane:
+//  * ballots of the bits of each lane's pair count give its exclusive prefix (mbcnt) and the
+//    wave's total; in each window of 64 pairs every owner marks its first pair's position in a
+//    128-byte per-wave LDS table, a ballot of the marks and a count-leading-zeros give each pair
+//    lane its segment's start, and one ds_bpermute from there its owner;
+//  * the pair lane fetches the owner's ray, leaf codes and current bound with ds_bpermute,
+//    loads the primitive's compact record and runs the fp32 pre-filter (sphere_maybe[_hi]);
+//  * each owner then reads back, with ds_bpermute, only the pairs that passed (a ballot mask,
+//    ascending = the leaf's primitive order), and applies exactly the sequential leaf_test rules (the pending-candidate
+//    rule of DEFER, or the exact fp64 test) with its CURRENT bound: a pair pre-filtered against
+//    the owner's older (larger) bound passes the current test iff lo <= the current bound,
+//    since lo and hi do not depend on the bound. Non-sphere primitives go to the owner's
+//    prim_candidate unchanged. So the (t, slot) minimum - the hit - is the sequential one.
+// bsrc: wave-uniform control flow only (every lane executes the bpermutes).
+// ---------------------------------------------------------------------------
+#ifndef RT_COOP_LEAF
+#define RT_COOP_LEAF 0
+#endif
+constexpr int kCoopNonSphere = 0x40000000;  // pair slot flag: not a sphere (the owner decides exactly)
+__device__ __forceinline__ int lane_prefix(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int bperm_i(int src, int v) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ float bperm_f(int src, float v) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+// The fields of FRay the sphere pre-filter reads (o, d, a, ia, dn), as make_fray computes them.
+__device__ __forceinline__ FRay fray_sphere(float ox, float oy, float oz, float dx, float dy, float dz) {
+    RT_FP32_FUSED
+    FRay f;
+    f.o[0] = ox; f.o[1] = oy; f.o[2] = oz;
+    f.d[0] = dx; f.d[1] = dy; f.d[2] = dz;
+    f.a = dx * dx + dy * dy + dz * dz;
+    f.ia = __builtin_amdgcn_rcpf(f.a);
+    f.dn = __builtin_amdgcn_sqrtf(f.a) * (1.0f + kRel);
+    return f;
+}
+
+template <class Real, bool COUNT, bool DEFER, bool PROF>
+__device__ __forceinline__ void coop_leaves(const DevScene& S, const FRay& f, const RayK<Real>& r, int la, int lb,
+                                            float& thi, Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt,
+                                            uint16_t* tab, Prof* pf) {
+    const int lane = (int)(threadIdx.x & (kWave - 1));
+    const int va = la != kTravDone ? ~la : 0;  // leaf code (first << 3 | count)
+    const int vb = lb != kTravDone ? ~lb : 0;
+    const int c = (va & 7) + (vb & 7);         // this lane's pairs, <= 14
+    int ex = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const unsigned long long m = __ballot((c >> b) & 1);
+        ex += lane_prefix(m) << b;
+        total += __popcll(m) << b;
+    }
+    const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
+    for (int base = 0; base < total; base += kWave) {  // (total: wave-uniform)
+        // window [base, base + 64) of the pair sequence: each owner whose pairs reach into it
+        // marks its first pair's position with (lane + 1, pairs before the window)
+        const int p0 = ex - base;
+        const bool in = c > 0 && p0 + c > 0 && p0 < kWave;
+        const int dst = max(p0, 0);
+        tab[lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (in) tab[dst] = (uint16_t)((lane + 1) | (max(-p0, 0) << 8));
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const int sv = tab[lane];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const unsigned long long starts = __ballot(sv != 0);
+        const unsigned long long below = starts & le;
+        const int sp0 = below ? 63 - __builtin_clzll(below) : 0;  // the nearest segment start at or below
+        const int so = bperm_i(sp0, sv);
+        const bool act = base + lane < total;
+        const int o = act ? (so & 0xff) - 1 : lane;
+        const int k = lane - sp0 + (so >> 8);  // pair index within the owner's leaves
+        const int va_o = bperm_i(o, va), vb_o = bperm_i(o, vb);
+        const float thi_o = bperm_f(o, thi);
+        const FRay fo = fray_sphere(bperm_f(o, f.o[0]), bperm_f(o, f.o[1]), bperm_f(o, f.o[2]), bperm_f(o, f.d[0]),
+                                    bperm_f(o, f.d[1]), bperm_f(o, f.d[2]));
+        float lo = __builtin_inff(), hi = __builtin_inff();
+        int slot = 0;
+        bool keep = false;  // the owner must look at this pair
+        if (act) {
+            if (PROF) pcount<PROF>(*pf, PR_LEAF);
+            const int ca_o = va_o & 7;
+            const int m = k < ca_o ? (va_o >> 3) + k : (vb_o >> 3) + (k - ca_o);
+            const float4 g = S.tsph[m];
+            slot = S.tprims[m];
+            if (g.w == g.w) {
+                if (COUNT) cnt[CT_SPHERE]++;
+                float l, h = __builtin_inff();
+                keep = DEFER ? sphere_maybe_hi(g, fo, thi_o, l, h) : sphere_maybe(g, fo, thi_o, l);
+                lo = l;
+                hi = h;
+            } else {
+                keep = true;  // not a sphere: the owner decides exactly (prim_candidate)
+                slot |= kCoopNonSphere;
+            }
+        }
+        // owners: the pairs they must look at, in the leaves' primitive order (ascending position)
+        const unsigned long long kept = __ballot(keep);
+        const int n_in = in ? min(p0 + c, kWave) - dst : 0;
+        unsigned long long cm = in ? (kept >> dst) & (n_in >= 64 ? ~0ull : ((1ull << n_in) - 1ull)) : 0ull;
+        while (__ballot(cm != 0ull) != 0ull) {
+            const int pos = cm ? dst + __builtin_ctzll(cm) : lane;
+            const float lk = bperm_f(pos, lo), hk = bperm_f(pos, hi);
+            const int sk = bperm_i(pos, slot);
+            if (cm) {
+                cm &= cm - 1ull;
+                if (sk & kCoopNonSphere) {
+                    const int ks = sk & ~kCoopNonSphere;
+                    Real t;
+                    if (prim_candidate<Real, COUNT>(S.prims[ks], ray_at_use<Real>(r), f, thi, t, cnt) &&
+                        (t < best_t || (t == best_t && ks < best))) {
+                        best_t = t;
+                        best = ks;
+                        thi = ::fminf(thi, upper_f<Real>(t));
+                    }
+                } else if (lk <= thi) {  // passes sphere_maybe[_hi] at the current bound
+                    if constexpr (DEFER) {
+                        if (pk >= 0 && !(hk < plo)) resolve_pending<Real, COUNT>(S, r, thi, best_t, best, pk, cnt);
+                        if (lk <= thi) {
+                            pk = sk;
+                            plo = lk;
+                            thi = ::fminf(thi, hk);
+                        }
+                    } else {
+                        if (COUNT) count_exact(cnt);
+                        Real t;
+                        if (sphere_t<Real>(S.prims[sk], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t) &&
+                            (t < best_t || (t == best_t && sk < best))) {
+                            best_t = t;
+                            best = sk;
+                            thi = ::fminf(thi, upper_f<Real>(t));
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 // Called by the whole wave with uniform control flow; lanes with `walking`
 // advance their walks. Returns when no lane walks, or (unless `drain`) after at
 // least one round once `min_ready` lanes of the wave are not walking.
-template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride>
+template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride, bool PF = false>
 __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, bool& walking,
                                                  int* stk, int min_ready, bool drain, uint32_t* cnt, Prof* pf = nullptr) {
     const FRay f = make_fray(o, d);
@@ -1160,11 +1328,59 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
     float* stkt = nullptr;
     (void)stkt;
     int rounds = 0;
+#if RT_COOP_LEAF
+    __shared__ uint16_t coop_tab[kBlockChunk / kWave][kWave];
+    uint16_t* tab = coop_tab[threadIdx.x / kWave];
+#endif
     while (true) {
         const unsigned long long wm = __ballot(walking);
         if (wm == 0ull) break;
         if (rounds > 0 && !drain && kWave - __popcll(wm) >= min_ready) break;
         ++rounds;
+#if RT_COOP_LEAF
+        int ref = W.ref, leaf = W.leaf, leaf2 = kTravDone;
+        int sp = W.sp;
+        float thi = W.thi;
+        auto pop = [&]() -> int {
+            if (sp > 0) {
+                --sp;
+                return stk[sp * STRIDE];
+            }
+            return kTravDone;
+        };
+        if (walking) {
+            while (ref >= 0) {
+                if (PROF) pcount<PROF>(*pf, PR_NODE);
+                if (COUNT) cnt[CT_NODE] += 4;
+                ref = t4_step<STRIDE>(S, ref, f, thi, stk, sp);
+                if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
+                    leaf = ref;
+                    ref = pop();
+                }
+                if (__ballot(leaf == kTravDone) == 0ull) break;  // every walking lane holds a leaf
+            }
+            if (PROF) psec<PROF>(*pf, PR_WNODE);
+            if (leaf == kTravDone && ref != kTravDone) {
+                leaf = ref;
+                ref = pop();
+            }
+            if (ref < 0 && ref != kTravDone) {  // the walk also stopped on a leaf: test it too
+                leaf2 = ref;
+                ref = pop();
+            }
+        }
+        coop_leaves<Real, COUNT, DEFER, PROF>(S, f, r, leaf, leaf2, thi, W.best_t, W.best, W.pk, W.plo, cnt, tab, pf);
+        if (PROF) psec<PROF>(*pf, PR_WLEAF);
+        if (walking) {
+            // a leaf popped last stays in W.ref: the next round's leaf phase takes it
+            W.ref = ref;
+            W.leaf = kTravDone;
+            W.sp = sp;
+            W.thi = thi;
+            if (ref == kTravDone) walking = false;
+        }
+        continue;
+#endif
         if (walking) {
             int sp = W.sp;
             float thi = W.thi;
@@ -1219,7 +1435,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             }
             while (leaf != kTravDone) {
                 if (PROF) pcount<PROF>(*pf, PR_LEAF);
-                leaf_test<Real, COUNT, DEFER>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
+                leaf_test<Real, COUNT, DEFER, PF>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
                 if (RT_WALK_LEAVES > 1 && leaf2 != kTravDone) {
                     leaf = leaf2;
@@ -2683,7 +2899,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
             psec<PROF>(pf, PR_RR);
             const bool was_walking = walking;
-            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF>(PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready,
+            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF, kStackStride,
+                             (RT_LEAF_PREFETCH == 2 || (RT_LEAF_PREFETCH == 1 && LDSS == 0))>(
+                PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready,
                                                                          exhausted, cnt, &pf);
             psec<PROF>(pf, PR_HIT);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)

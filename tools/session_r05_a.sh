@@ -1,0 +1,10 @@
+set -o pipefail
+bash tools/gpu_run.sh r05_a sections:spheres sections:spheres100k || exit $?
+RT_AMD_VARIANT=coop bash tools/gpu_run.sh r05_c "pytest:ref_precision_matches_oracle or fast_traversal_equals or reference_bvh_and_list or sah_tree or chunked_kernel_equals or large_scene_global or full_size_config_rows or random_scenes or edge_cases or config1 or tiny_scenes" || exit $?
+export CFGS="sph --scene spheres --spp 64 --depth 8
+s100k --scene spheres100k --width 2048 --spp 16 --depth 100
+rain --scene rain --width 1920 --spp 128 --depth 16"
+export ARMS="base -
+coop coop"
+bash tools/gpu_run.sh r05_a abvar || exit $?
+RT_AMD_VARIANT=coop bash tools/gpu_run.sh r05_c sections:spheres sections:spheres100k || exit $?
