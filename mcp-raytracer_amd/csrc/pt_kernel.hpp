@@ -64,6 +64,8 @@ struct DevScene {
     int32_t n_top;                      // launches walking the tree from global memory: nodes [0, n_top)
                                         // (breadth-first: the tree's top) have a padded copy in LDS
     const char* top_lds;                // ... after the traversal stack (scene_view; LDSS 0 only)
+    const RtQ4Node* __restrict__ qnodes; // the tree's compressed 4-wide nodes (global), or null
+    int32_t qtree;                      // LDSS 0 launch walking qnodes (and caching their top in LDS)
     int32_t nearfar;                    // 4-wide node step picks near / far rows by the ray's signs (t4_step);
                                         // scene_view sets a constant per LDS level (see there)
     int32_t troot;                      // fast traversal root reference
@@ -740,8 +742,79 @@ __device__ __forceinline__ void t4_rows(const void* nd0, const FRay& f, bool nf,
 //    goes past sp + 2: at a node of level L (root 1) the stack holds at most 3 (L - 1)
 //    entries (3 per ancestor), so writes stay below 3 t4depth <= stack_depth - 2 entries
 //    (scene.cpp: stack_depth = max(..., 3 t4depth + 1) + 1).
+// The pair sort and stack pushes of a 4-wide node step (below): keys k (entry-distance bits, ~0
+// for a miss), child references r, n hit children.
+template <int STRIDE>
+__device__ __forceinline__ int t4_push(uint32_t (&k)[4], int (&r)[4], int n, int* stk, int& sp) {
+    auto cx = [&](int i, int j) {
+        const bool sw = k[j] < k[i];
+        const uint32_t lo = min(k[i], k[j]), hi = max(k[i], k[j]);
+        const int ri = r[i], rj = r[j];
+        k[i] = lo;
+        k[j] = hi;
+        r[i] = sw ? rj : ri;
+        r[j] = sw ? ri : rj;
+    };
+    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+    const int popped = stk[max(sp - 1, 0) * STRIDE];
+#pragma unroll
+    for (int j = 3; j >= 1; --j) stk[max(sp + n - 1 - j, sp) * STRIDE] = r[j];
+    const int next = n > 0 ? r[0] : (sp > 0 ? popped : kT4Empty);  // (kT4Empty = kTravDone)
+    sp = n > 0 ? sp + n - 1 : max(sp - 1, 0);
+    return next;
+}
+
+// One step of the 4-wide walk over compressed nodes (RtQ4Node; LDSS 0 launches with S.qtree):
+// the same slab test and push order as t4_step on boxes decoded exactly from the 8-bit grid
+// (fma(q, scl, org) is exact by construction, scene.cpp make_q4nodes) - boxes that contain the
+// 128-byte node's, so the walk stays conservative and the (t, slot) minimum unchanged. Half the
+// bytes per node: 4 row loads instead of 7, and twice the nodes in the LDS top cache (80-byte
+// stride there: 20 i + 4 r covers 16 bank windows for i mod 16).
+constexpr int kQ4LdsStride = (int)sizeof(RtQ4Node) + 16;
+template <int STRIDE>
+__device__ __forceinline__ int q4_step(const DevScene& S, int ref, const FRay& f, float thi, int* stk, int& sp) {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    v4 h0, h1, h2, h3;
+    if (ref < S.n_top) {
+        typedef const __attribute__((address_space(3))) v4* P4;
+        const P4 b = (P4)__builtin_assume_aligned(S.top_lds + (size_t)ref * kQ4LdsStride, 16);
+        h0 = b[0]; h1 = b[1]; h2 = b[2]; h3 = b[3];
+    } else {
+        typedef const __attribute__((address_space(1))) v4* P4;
+        const P4 b = (P4)__builtin_assume_aligned(S.qnodes + ref, 16);
+        h0 = b[0]; h1 = b[1]; h2 = b[2]; h3 = b[3];
+    }
+    const float org[3] = {h0.x, h0.y, h0.z};
+    const float scl[3] = {h0.w, h1.x, h1.y};
+    const uint32_t qlo[3] = {__float_as_uint(h1.z), __float_as_uint(h1.w), __float_as_uint(h2.x)};
+    const uint32_t qhi[3] = {__float_as_uint(h2.y), __float_as_uint(h2.z), __float_as_uint(h2.w)};
+    const int cr[4] = {__float_as_int(h3.x), __float_as_int(h3.y), __float_as_int(h3.z), __float_as_int(h3.w)};
+    uint32_t k[4];
+    int r[4];
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float tn = kTminLo, tf = thi;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float lo = __builtin_fmaf((float)((qlo[a] >> (8 * c)) & 255u), scl[a], org[a]);
+            const float hi = __builtin_fmaf((float)((qhi[a] >> (8 * c)) & 255u), scl[a], org[a]);
+            const float t0 = slab_t(lo, f, a);
+            const float t1 = slab_t(hi, f, a);
+            tn = ::fmaxf(tn, ::fminf(t0, t1));
+            tf = ::fminf(tf, ::fmaxf(t0, t1));
+        }
+        const bool hit = (cr[c] != kT4Empty) & slab_accept(tn, tf, f);
+        k[c] = hit ? __float_as_uint(tn) : ~0u;
+        r[c] = cr[c];
+        n += hit ? 1 : 0;
+    }
+    return t4_push<STRIDE>(k, r, n, stk, sp);
+}
+
 template <int STRIDE>
 __device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f, float thi, int* stk, int& sp) {
+    if (S.qtree) return q4_step<STRIDE>(S, ref, f, thi, stk, sp);
     T4Rows R;
     const bool nf = RT_NEARFAR && S.nearfar;
     if (ref < S.n_top) t4_rows<3>(S.top_lds + (size_t)ref * (sizeof(RtT4Node) + 16), f, nf, R);
@@ -778,22 +851,7 @@ __device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f
         r[c] = cr[c];
         n += hit ? 1 : 0;
     }
-    auto cx = [&](int i, int j) {
-        const bool sw = k[j] < k[i];
-        const uint32_t lo = min(k[i], k[j]), hi = max(k[i], k[j]);
-        const int ri = r[i], rj = r[j];
-        k[i] = lo;
-        k[j] = hi;
-        r[i] = sw ? rj : ri;
-        r[j] = sw ? ri : rj;
-    };
-    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-    const int popped = stk[max(sp - 1, 0) * STRIDE];
-#pragma unroll
-    for (int j = 3; j >= 1; --j) stk[max(sp + n - 1 - j, sp) * STRIDE] = r[j];
-    const int next = n > 0 ? r[0] : (sp > 0 ? popped : kT4Empty);  // (kT4Empty = kTravDone)
-    sp = n > 0 ? sp + n - 1 : max(sp - 1, 0);
-    return next;
+    return t4_push<STRIDE>(k, r, n, stk, sp);
 }
 
 // fp32 pre-filters: false only when the exact test surely gives no t <= thi.
@@ -2403,6 +2461,7 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
     // scratch spills and spheres-100k lost 2.3 % (profiles/r04/nearfar/). A constant per level, so
     // the unused form folds away.
     S.nearfar = LDSS > 0 ? 1 : 0;
+    if (LDSS > 0) S.qtree = 0;  // (compressed nodes: trees walked from global memory only)
     if (LDSS == 0) S.top_lds = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
     if (LDSS > 0) {
         S.n_top = 0;  // the whole tree is in LDS (a constant: the walk's reads stay ds_read)
@@ -2430,9 +2489,14 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
 // from the global copy.)
 template <int LDSS>
 __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
-    if (LDSS == 0 && S0.n_top > 0) {  // the tree's top: n_top nodes of 8 rows, a pad row each
+    if (LDSS == 0 && S0.n_top > 0) {  // the tree's top: n_top nodes of 8 (compressed: 4) rows, a pad row each
         uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
-        for (int w = threadIdx.x; w < S0.n_top * 8; w += blockDim.x) dst[w + (w >> 3)] = S0.blob[w];
+        if (S0.qtree) {
+            const uint4* src = reinterpret_cast<const uint4*>(S0.qnodes);
+            for (int w = threadIdx.x; w < S0.n_top * 4; w += blockDim.x) dst[w + (w >> 2)] = src[w];
+        } else {
+            for (int w = threadIdx.x; w < S0.n_top * 8; w += blockDim.x) dst[w + (w >> 3)] = S0.blob[w];
+        }
         __syncthreads();
     }
     if (LDSS > 0) {
@@ -2760,6 +2824,9 @@ __device__ __forceinline__ void take_pool(const RenderOut& out, const SampleBuf&
     pool_end = min(base + sb.pool, sb.n_items);
 }
 
+#ifndef RT_DEFER_DIFFUSE
+#define RT_DEFER_DIFFUSE 0  // chunked kernel, resumable walks: diffuse shading batched to >= this many lanes
+#endif
 #ifndef RT_CHUNK_KOPQ
 #define RT_CHUNK_KOPQ 1  // 0: the A/B arm that keeps the launch parameters in SGPRs (profiles/r03/exp5_ckopq/)
 #endif
@@ -2827,6 +2894,11 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     FastWalk<Real> W;
     bool walking = false;
     LaneBounces lb;  // SampleBuf::rec12
+    // RT_DEFER_DIFFUSE (> 0, no emission stack): a path whose hit scatters diffusely waits for its
+    // light sampling until that many lanes of the wave do (pend_h: h | planar << 14 | front << 15,
+    // pend_mat: the Lambertian material; -1 = none)
+    constexpr int kDeferD = (RT_DEFER_DIFFUSE > 0 && !EMIT && RS) ? RT_DEFER_DIFFUSE : 0;
+    int pend_h = -1, pend_mat = 0;
 
 #if RT_CHUNK_KOPQ
 #define PK_SB (kern_args().sb)
@@ -2883,7 +2955,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             prof_trip<PROF>(pf);
             // lanes between rays: start a path if needed, then the level's depth
             // cut-off / roulette, and the walk of its ray
-            if (slot >= 0 && !walking) {
+            if (slot >= 0 && !walking && (!kDeferD || pend_h < 0)) {
                 if (new_path) {
                     path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(PK_SB.s_base + s));
                     new_path = false;
@@ -2908,7 +2980,53 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             if (was_walking && !walking) {
                 fast_walk_resolve<Real, COUNT>(PK_S, P.o, P.d, W, cnt);
                 V3 c;
-                if (path_post<Real, EMIT, COUNT, PROF>(PK_S, C, P, W.best, W.best_t, cnt, st_err, pf, c)) finish_sample(c);
+                if constexpr (kDeferD) {
+                    // path_post up to the diffuse shading, which waits for its batch (below)
+                    const int h = W.best;
+                    if (h < 0) {
+                        finish_sample(miss_color<Real, EMIT, PROF>(C, P, st_err, pf));
+                    } else {
+                        V3 p, nrm, emitted, att, sdir;
+                        bool front, planar;
+                        int dmat = 0;
+                        const int kind = shade_hit<Real, EMIT, COUNT, PROF>(PK_S, P, h, W.best_t, cnt, pf, p, nrm, front,
+                                                                            planar, emitted, att, sdir, &dmat);
+                        if (kind == SC_NONE) {
+                            finish_sample(emitted);
+                        } else {
+                            ++P.bounces;
+                            P.o = p;
+                            if (kind == SC_SPEC) {
+                                P.T = mulv(P.T, att);
+                                P.d = sdir;
+                            } else {
+                                P.d = nrm;  // (as the pool kernel's D queue: the face normal rides in d)
+                                pend_h = h | (planar ? (1 << 14) : 0) | (front ? (1 << 15) : 0);
+                                pend_mat = dmat;
+                            }
+                        }
+                    }
+                } else {
+                    if (path_post<Real, EMIT, COUNT, PROF>(PK_S, C, P, W.best, W.best_t, cnt, st_err, pf, c))
+                        finish_sample(c);
+                }
+            }
+            if constexpr (kDeferD) {
+                // RT_DEFER_DIFFUSE: the mixture-PDF light sampling of the paths that wait for it, once
+                // kDeferD of them do (or no walk is left to overlap with): the same shade_diffuse call
+                // path_post makes, later - no draw of the path happens in between, so the draw order
+                // and the result are path_post's
+                const unsigned long long pm = __ballot(pend_h >= 0);
+                if (pm != 0ull && (__popcll(pm) >= kDeferD || exhausted || __ballot(walking) == 0ull)) {
+                    if (pend_h >= 0) {
+                        const int h = pend_h & 0x3fff;
+                        const V3 att = ld3(PK_S.mats[pend_mat].color);  // the Lambertian scatter's attenuation
+                        if (shade_diffuse<Real, EMIT, COUNT, PROF, 0>(PK_S, C, P, h, (pend_h >> 14) & 1,
+                                                                      (pend_h >> 15) & 1, P.o, P.d, att, cnt, pf))
+                            finish_sample(mulv(ld3(PK_S.mats[PK_S.prims[h].mat].emitted), P.T));
+                        pend_h = -1;
+                    }
+                }
             }
             psec<PROF>(pf, PR_ACC);
         } else if (slot >= 0) {

@@ -81,6 +81,10 @@ int device_cus(int dev) {
 // the smallest of: the units left, the record budget, and the counter headroom - a larger
 // record budget gives fewer, bounded passes instead of an error.
 constexpr long kItemCap = (1l << 31) - (1l << 22);
+#ifndef RT_QNODES_DEFAULT
+#define RT_QNODES_DEFAULT 0
+#endif
+constexpr bool kQnodesDefault = RT_QNODES_DEFAULT != 0;
 long pass_units(long units_left, long unit_slots, long chunks_per_slot, size_t rec_bytes_per_unit, size_t budget) {
     const long by_budget = (long)(budget / std::max<size_t>(rec_bytes_per_unit, 1));
     const long by_items = (kItemCap - 1) / (std::max<long>(unit_slots, 1) * std::max<long>(chunks_per_slot, 1));
@@ -136,6 +140,7 @@ struct rt_camera {
     int32_t lds_words = 0;    // [tnodes][tprims][tsph][prims] prefix, 16-byte words
     int32_t lds_words2 = 0;   // the same + [mats][lights]
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
+    int32_t off_q4 = -1;  // compressed 4-wide nodes (RtQ4Node) in the blob, or -1
     int32_t off_pre = 0;
     int32_t n_onb = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
@@ -246,6 +251,8 @@ struct rt_camera {
         lds_words2 = (int32_t)(blob.size() / 16);
         append(blob, build.nodes, &off_nodes);
         append(blob, prefilter_records(build.prims), &off_pre);
+        off_q4 = -1;
+        if (RT_BVH4 && !build.q4nodes.empty()) append(blob, build.q4nodes, &off_q4);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
         if (!blob.empty()) hip_check(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice), "hipMemcpy");
         hip_check(hipMalloc(&d_stats, ST_WORDS * kStatStride * sizeof(unsigned long long)), "hipMalloc");
@@ -302,6 +309,8 @@ struct rt_camera {
         S.n_onb = n_onb;
         S.off_onbs = off_onbs;
         S.blob = d_blob;
+        S.qnodes = off_q4 >= 0 ? reinterpret_cast<const RtQ4Node*>(b + off_q4) : nullptr;
+        S.qtree = 0;
         S.lds_words = lds_words;
         S.off_prims = off_prims;
         S.off_mats = off_mats;
@@ -361,10 +370,15 @@ struct rt_camera {
         g.lds_bytes = stack + (g.lds_level == 0 ? 0 : (size_t)((g.lds_level == 2 ? lds_words2 : lds_words) + node_pad) * 16);
         // a tree walked from global memory: its top (breadth-first prefix) in the LDS left beside the stack
         int32_t n_top = 0;
+        // a tree walked from global memory walks its compressed nodes (RtQ4Node: half the bytes per
+        // node, twice the nodes in the LDS top cache) where it has them; RT_AMD_QNODES=0/1 overrides
+        const bool qtree = g.lds_level == 0 && RT_BVH4 && v.trav == TRAV_FAST && off_q4 >= 0 &&
+                           env_flag("RT_AMD_QNODES", kQnodesDefault);
+        const size_t node_lds = qtree ? (size_t)kQ4LdsStride : sizeof(RtT4Node) + 16;
         if (g.lds_level == 0 && RT_BVH4 && v.trav == TRAV_FAST && lds_scene_enabled() && env_flag("RT_AMD_TOP_CACHE", true)) {
             const size_t room = lds_cap > stack ? lds_cap - stack : 0;
-            n_top = (int32_t)std::min<size_t>(build.t4nodes.size(), room / (sizeof(RtT4Node) + 16));
-            g.lds_bytes = stack + (size_t)n_top * (sizeof(RtT4Node) + 16);
+            n_top = (int32_t)std::min<size_t>(build.t4nodes.size(), room / node_lds);
+            g.lds_bytes = stack + (size_t)n_top * node_lds;
         }
         // Deferred exact sphere tests pay where the walk is VALU-bound and leaves hold
         // several candidates: LDS-resident trees of >= 100 primitives (spheres-500
@@ -393,6 +407,7 @@ struct rt_camera {
         S.lds_words = g.lds_level == 2 ? lds_words2 : lds_words;
         S.lds_node_pad = g.lds_level > 0 ? node_pad : 0;
         S.n_top = n_top;
+        S.qtree = qtree ? 1 : 0;
         // Fixed spp: the chunked / pool kernels (per-sample records, in-order accumulate)
         // at every size. Round 1 kept the sequential kernel for images of >= 4 tiles per
         // resident wave; with the hand-out rules above the chunked kernel is faster there

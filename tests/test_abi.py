@@ -245,3 +245,15 @@ def test_pass_plan_caps_items_at_the_counter_headroom(rt):
     assert plan(10, 64, 16, 1 << 20, 1) == 1
     with pytest.raises(_lib.RtError):
         plan(10, 0, 16, 1000, 1 << 30)
+
+
+def test_compressed_nodes_build_for_sphere_trees(rt):
+    """make_q4nodes (scene.cpp) quantises every 4-wide node's child boxes to 8-bit grids and
+    asserts on the host that each decoded box (an exact fp32 fma) contains the node's box -
+    camera creation throws otherwise. Sphere fields of several sizes and seeds, incl. one
+    whose tree is walked from global memory (the compressed nodes' use)."""
+    for count, seed in ((50, 1), (500, 42), (6000, 9), (20000, 5)):
+        sd = rt.generate_scene_data({"type": "spheres", "options": {"count": count, "seed": seed}})
+        cam = rt.create_camera_from_scene_data(sd, {"width": 16, "samples": 1, "aTolerance": 0})
+        assert cam.info["n_objects"] >= 1
+        cam.close()

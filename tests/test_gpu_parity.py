@@ -586,11 +586,14 @@ def test_large_scene_global_traversal(rt, oracle, gpu, monkeypatch):
     sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 6000, "seed": 9}})
     ro = {"width": 96, "aspect": 1, "samples": 8, "depth": 12, **NOADAPT}
     outs = []
-    for trav, defer in (("reference", "0"), ("fast", "0"), ("fast", "1")):
+    # (the fast walks both on the 128-byte 4-wide nodes and on the compressed 64-byte ones)
+    for trav, defer, q in (("reference", "0", "0"), ("fast", "0", "0"), ("fast", "1", "0"), ("fast", "0", "1"),
+                           ("fast", "1", "1")):
         monkeypatch.setenv("RT_AMD_DEFER", defer)
+        monkeypatch.setenv("RT_AMD_QNODES", q)
         cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
         outs.append((rgb, rad, st))
-    for k in (1, 2):
+    for k in range(1, len(outs)):
         assert np.array_equal(outs[0][0], outs[k][0])
         assert np.array_equal(outs[0][1], outs[k][1], equal_nan=True)
         assert outs[0][2].bounces == outs[k][2].bounces
