@@ -65,6 +65,8 @@ struct DevScene {
                                         // (breadth-first: the tree's top) have a padded copy in LDS
     const char* top_lds;                // ... after the traversal stack (scene_view; LDSS 0 only)
     const RtQ4Node* __restrict__ qnodes; // the tree's compressed 4-wide nodes (global), or null
+    const RtLeafSph* __restrict__ tsph2; // trees walked from global memory: leaf-order sphere records with
+                                         // the fp64 radius and the slot (one load per exact test), or null
     int32_t qtree;                      // LDSS 0 launch walking qnodes (and caching their top in LDS)
     int32_t nearfar;                    // 4-wide node step picks near / far rows by the ray's signs (t4_step);
                                         // scene_view sets a constant per LDS level (see there)
@@ -325,9 +327,7 @@ template <> __device__ __forceinline__ float plane_d<float>(const RtPrim& p) { r
 
 // Sphere.hit root selection (src/entities/sphere.ts:45-65); returns t only.
 template <class Real>
-__device__ __forceinline__ bool sphere_t(const RtPrim& p, const RayK<Real>& r, Real tmin, Real tmax, Real& t) {
-    const V3 c = ld3(p.g0);
-    const Real rad = sphere_radius<Real>(p);
+__device__ __forceinline__ bool sphere_t_cr(V3 c, Real rad, const RayK<Real>& r, Real tmin, Real tmax, Real& t) {
     const V3 oc = sub(r.o, c);
     const Real halfB = dot<Real>(oc, r.d);
     const Real cc = len2<Real>(oc) - rad * rad;
@@ -341,6 +341,10 @@ __device__ __forceinline__ bool sphere_t(const RtPrim& p, const RayK<Real>& r, R
     }
     t = root;
     return true;
+}
+template <class Real>
+__device__ __forceinline__ bool sphere_t(const RtPrim& p, const RayK<Real>& r, Real tmin, Real tmax, Real& t) {
+    return sphere_t_cr<Real>(ld3(p.g0), sphere_radius<Real>(p), r, tmin, tmax, t);
 }
 
 // Plane.intersect (src/entities/plane.ts:55-77) + Quad bounds (quad.ts:50-76).
@@ -699,7 +703,9 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 // branches, so each stays a ds_read / global_load - one generic pointer made them flat loads,
 // 3.5 % slower on spheres-100k).
 __device__ __forceinline__ const RtT4Node* t4_node(const DevScene& S, int ref) {
-    return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) + (size_t)ref * S.t4_stride);
+    // (a 24-bit multiply, full rate: node indices stay below 2^24, scene.cpp make_t4nodes)
+    return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) +
+                                             (size_t)__umul24((unsigned)ref, (unsigned)S.t4_stride));
 }
 struct T4Rows {
     float4 nr[3], fr[3];  // per axis: the four children's near-plane / far-plane coordinates
@@ -1034,35 +1040,27 @@ __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Re
     }
 }
 
-// RT_LEAF_PREFETCH: a leaf's compact records (tsph) and leaf slots (tprims) are loaded for up to
-// four primitives at once, before the first pre-filter, so a leaf costs one memory latency instead
-// of one per primitive (trees walked from global memory: every tsph / tprims read is an L2 round
-// trip). Entries past the leaf's end read the records that follow it - the next leaf's, or the
-// next blob section's (tprims is followed by tsph, tsph by prims) - and are never used.
-// 0: off, 1: trees walked from global memory (LDSS 0), 2: every fast-traversal launch.
-#ifndef RT_LEAF_PREFETCH
-#define RT_LEAF_PREFETCH 0
-#endif
-template <class Real, bool COUNT, bool DEFER, bool PF = false>
+// A leaf's primitives in leaf order: the fp32 pre-filter from the compact leaf-order record, then
+// the exact test (or, with DEFER, the pending-candidate rule). Trees walked from global memory
+// (S.tsph2) read one 32-byte record per primitive that also carries the fp64 radius and the slot,
+// so a sphere's exact test needs no dependent tprims -> RtPrim load (two L2 round trips).
+// (Round 5 also tried loading a leaf's four records before its first test: spheres-100k
+// 37.1 -> 44.8 ms, spheres-500 +0 %, profiles/r05/coop_v2_prefetch/ - dropped.)
+template <class Real, bool COUNT, bool DEFER>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
                                           Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt) {
     const int v = ~ref;
     const int first = v >> 3;
     const int end = first + (v & 7);
-    float4 gq[PF ? 4 : 1];
-    int kq[PF ? 4 : 1];
     for (int m = first; m < end; ++m) {
-        const int j = (m - first) & 3;
-        if constexpr (PF) {
-            if (j == 0) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    gq[u] = S.tsph[m + u];
-                    kq[u] = S.tprims[m + u];
-                }
-            }
+        RtLeafSph q;
+        float4 g;
+        if (!DEFER && S.tsph2) {
+            q = S.tsph2[m];
+            g = make_float4(q.c[0], q.c[1], q.c[2], q.r32);
+        } else {
+            g = S.tsph[m];
         }
-        const float4 g = PF ? gq[j] : S.tsph[m];
         Real t;
         int k;  // reference leaf slot (the tie-break key)
         bool cand;
@@ -1072,7 +1070,7 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
             if constexpr (DEFER) {
             float hi;
             if (!sphere_maybe_hi(g, f, thi, lo, hi)) continue;
-            k = PF ? kq[j] : S.tprims[m];
+            k = S.tprims[m];
             // a second candidate: one surely hit before the pending one's lower bound
             // replaces it untested (t_new <= hi < plo <= t_pending); otherwise the
             // pending one is settled first
@@ -1086,11 +1084,17 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
             } else {
             if (!sphere_maybe(g, f, thi, lo)) continue;
             if (COUNT) count_exact(cnt);
-            k = PF ? kq[j] : S.tprims[m];
-            cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
+            if (S.tsph2) {
+                k = q.slot;
+                cand = sphere_t_cr<Real>(v3(q.c[0], q.c[1], q.c[2]), sizeof(Real) == 8 ? (Real)q.r64 : (Real)q.r32,
+                                         ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
+            } else {
+                k = S.tprims[m];
+                cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
+            }
             }
         } else {
-            k = PF ? kq[j] : S.tprims[m];
+            k = (!DEFER && S.tsph2) ? q.slot : S.tprims[m];
             cand = prim_candidate<Real, COUNT>(S.prims[k], ray_at_use<Real>(r), f, thi, t, cnt);
         }
         if (cand && (t < best_t || (t == best_t && k < best))) {
@@ -1378,7 +1382,7 @@ __device__ __forceinline__ void coop_leaves(const DevScene& S, const FRay& f, co
 // Called by the whole wave with uniform control flow; lanes with `walking`
 // advance their walks. Returns when no lane walks, or (unless `drain`) after at
 // least one round once `min_ready` lanes of the wave are not walking.
-template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride, bool PF = false>
+template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride>
 __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, bool& walking,
                                                  int* stk, int min_ready, bool drain, uint32_t* cnt, Prof* pf = nullptr) {
     const FRay f = make_fray(o, d);
@@ -1493,7 +1497,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             }
             while (leaf != kTravDone) {
                 if (PROF) pcount<PROF>(*pf, PR_LEAF);
-                leaf_test<Real, COUNT, DEFER, PF>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
+                leaf_test<Real, COUNT, DEFER>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
                 if (RT_WALK_LEAVES > 1 && leaf2 != kTravDone) {
                     leaf = leaf2;
@@ -2461,7 +2465,10 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
     // scratch spills and spheres-100k lost 2.3 % (profiles/r04/nearfar/). A constant per level, so
     // the unused form folds away.
     S.nearfar = LDSS > 0 ? 1 : 0;
-    if (LDSS > 0) S.qtree = 0;  // (compressed nodes: trees walked from global memory only)
+    if (LDSS > 0) {
+        S.qtree = 0;  // (compressed nodes and fp64 leaf records: trees walked from global memory only)
+        S.tsph2 = nullptr;
+    }
     if (LDSS == 0) S.top_lds = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
     if (LDSS > 0) {
         S.n_top = 0;  // the whole tree is in LDS (a constant: the walk's reads stay ds_read)
@@ -2971,9 +2978,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
             psec<PROF>(pf, PR_RR);
             const bool was_walking = walking;
-            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF, kStackStride,
-                             (RT_LEAF_PREFETCH == 2 || (RT_LEAF_PREFETCH == 1 && LDSS == 0))>(
-                PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready,
+            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF>(PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready,
                                                                          exhausted, cnt, &pf);
             psec<PROF>(pf, PR_HIT);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)

@@ -85,6 +85,10 @@ constexpr long kItemCap = (1l << 31) - (1l << 22);
 #define RT_QNODES_DEFAULT 0
 #endif
 constexpr bool kQnodesDefault = RT_QNODES_DEFAULT != 0;
+#ifndef RT_TSPH2_DEFAULT
+#define RT_TSPH2_DEFAULT 0
+#endif
+constexpr bool kTsph2Default = RT_TSPH2_DEFAULT != 0;
 long pass_units(long units_left, long unit_slots, long chunks_per_slot, size_t rec_bytes_per_unit, size_t budget) {
     const long by_budget = (long)(budget / std::max<size_t>(rec_bytes_per_unit, 1));
     const long by_items = (kItemCap - 1) / (std::max<long>(unit_slots, 1) * std::max<long>(chunks_per_slot, 1));
@@ -141,6 +145,7 @@ struct rt_camera {
     int32_t lds_words2 = 0;   // the same + [mats][lights]
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
     int32_t off_q4 = -1;  // compressed 4-wide nodes (RtQ4Node) in the blob, or -1
+    int32_t off_tsph2 = -1;  // leaf-order sphere records with the fp64 radius (RtLeafSph), or -1
     int32_t off_pre = 0;
     int32_t n_onb = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
@@ -253,6 +258,8 @@ struct rt_camera {
         append(blob, prefilter_records(build.prims), &off_pre);
         off_q4 = -1;
         if (RT_BVH4 && !build.q4nodes.empty()) append(blob, build.q4nodes, &off_q4);
+        off_tsph2 = -1;
+        if (!build.tsph2.empty()) append(blob, build.tsph2, &off_tsph2);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
         if (!blob.empty()) hip_check(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice), "hipMemcpy");
         hip_check(hipMalloc(&d_stats, ST_WORDS * kStatStride * sizeof(unsigned long long)), "hipMalloc");
@@ -310,6 +317,7 @@ struct rt_camera {
         S.off_onbs = off_onbs;
         S.blob = d_blob;
         S.qnodes = off_q4 >= 0 ? reinterpret_cast<const RtQ4Node*>(b + off_q4) : nullptr;
+        S.tsph2 = nullptr;  // (set per launch: trees walked from global memory)
         S.qtree = 0;
         S.lds_words = lds_words;
         S.off_prims = off_prims;
@@ -408,6 +416,11 @@ struct rt_camera {
         S.lds_node_pad = g.lds_level > 0 ? node_pad : 0;
         S.n_top = n_top;
         S.qtree = qtree ? 1 : 0;
+        // trees walked from global memory: leaf records that carry the exact test's fp64 radius
+        // (RT_AMD_TSPH2=0/1 overrides)
+        S.tsph2 = g.lds_level == 0 && v.trav == TRAV_FAST && off_tsph2 >= 0 && env_flag("RT_AMD_TSPH2", kTsph2Default)
+                      ? reinterpret_cast<const RtLeafSph*>(reinterpret_cast<const char*>(d_blob) + off_tsph2)
+                      : nullptr;
         // Fixed spp: the chunked / pool kernels (per-sample records, in-order accumulate)
         // at every size. Round 1 kept the sequential kernel for images of >= 4 tiles per
         // resident wave; with the hand-out rules above the chunked kernel is faster there

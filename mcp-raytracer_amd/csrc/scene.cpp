@@ -1071,6 +1071,7 @@ std::vector<RtT4Node> make_t4nodes(const std::vector<RtNode>& f, int32_t& root_r
     if (f.empty()) { root_ref = ~0; return out; }
     if (f[0].b < 0) { root_ref = t4_leaf_ref(f[0]); return out; }
     root_ref = t4_build(f, 0, 1, out, depth);  // the root is node 0 (pre-order)
+    if (out.size() >= (1u << 24)) throw std::runtime_error("4-wide tree: more than 2^24 nodes");  // (t4_node: 24-bit multiply)
     return t4_breadth_first(out);
 }
 
@@ -1415,10 +1416,19 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
         // leaf-order sphere records for the fp32 pre-filter: contiguous per leaf and
         // a quarter of a primitive record, so large scenes stay cache-resident
         b.out.tsph.assign(b.out.tprims.size() * 4, std::numeric_limits<float>::quiet_NaN());
+        b.out.tsph2.assign(b.out.tprims.size(), RtLeafSph{});
         for (size_t m = 0; m < b.out.tprims.size(); ++m) {
             const RtPrim& p = b.out.prims[(size_t)b.out.tprims[m]];
-            if (p.type == PRIM_SPHERE)
+            RtLeafSph& q = b.out.tsph2[m];
+            q.slot = b.out.tprims[m];
+            for (int c = 0; c < 3; ++c) q.c[c] = std::numeric_limits<float>::quiet_NaN();
+            q.r32 = std::numeric_limits<float>::quiet_NaN();
+            if (p.type == PRIM_SPHERE) {
                 for (int c = 0; c < 4; ++c) b.out.tsph[m * 4 + c] = p.g0[c];
+                for (int c = 0; c < 3; ++c) q.c[c] = p.g0[c];
+                q.r32 = p.g0[3];
+                q.r64 = p.s0;  // the JS double radius (sphere_radius<double>)
+            }
         }
     }
     // stack entries: reference DFS (depth + 1), binary fast tree (depth + 1),

@@ -90,6 +90,18 @@ static_assert(sizeof(RtQ4Node) == 64, "RtQ4Node must be 64 bytes");
 // an infinite bound (planes) - the tree then keeps its 128-byte nodes only.
 bool make_q4nodes(const std::vector<struct RtT4Node>& t4, std::vector<RtQ4Node>& out);
 
+// Leaf-order sphere record for trees walked from global memory (tsph2, per tprims entry): the
+// fp32 pre-filter's {centre, fp32 radius}, the exact test's fp64 radius (the JS double) and the
+// leaf slot - the exact Sphere.hit needs no dependent RtPrim load. Non-spheres: NaN centre.
+struct alignas(16) RtLeafSph {
+    float c[3];
+    float r32;
+    double r64;
+    int32_t slot;
+    int32_t pad;
+};
+static_assert(sizeof(RtLeafSph) == 32, "RtLeafSph must be 32 bytes");
+
 struct alignas(16) RtPrim {
     int32_t type;
     int32_t mat;
@@ -191,6 +203,7 @@ struct SceneBuild {
     std::vector<RtTNode> tnodes; // fast-traversal tree, children-in-parent (SAH, or the reference tree)
     std::vector<int32_t> tprims; // its leaves' primitive slots (padded to a multiple of 4)
     std::vector<float> tsph;     // per tprims entry: sphere {centre, fp32 radius}, NaNs for other types
+    std::vector<RtLeafSph> tsph2; // per tprims entry: the same + fp64 radius + slot (trees walked from global memory)
     std::vector<RtT4Node> t4nodes; // the same tree collapsed to 4-wide nodes (RT_BVH4)
     std::vector<RtQ4Node> q4nodes; // ... quantised (empty when some bound is infinite)
     int32_t t4root = 0;          // its root reference
