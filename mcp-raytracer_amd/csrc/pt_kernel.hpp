@@ -702,10 +702,16 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 // in LDS beside the stack (t4_step reads a node from there or from global memory: two loads in two
 // branches, so each stays a ds_read / global_load - one generic pointer made them flat loads,
 // 3.5 % slower on spheres-100k).
+#ifndef RT_UMUL24
+#define RT_UMUL24 1
+#endif
 __device__ __forceinline__ const RtT4Node* t4_node(const DevScene& S, int ref) {
-    // (a 24-bit multiply, full rate: node indices stay below 2^24, scene.cpp make_t4nodes)
+#if RT_UMUL24  // (a 24-bit multiply, full rate: node indices stay below 2^24, scene.cpp make_t4nodes)
     return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) +
                                              (size_t)__umul24((unsigned)ref, (unsigned)S.t4_stride));
+#else
+    return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) + (size_t)ref * S.t4_stride);
+#endif
 }
 struct T4Rows {
     float4 nr[3], fr[3];  // per axis: the four children's near-plane / far-plane coordinates

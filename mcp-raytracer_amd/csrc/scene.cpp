@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <random>
@@ -1089,6 +1090,16 @@ struct SahBuilder {
     std::vector<RtNode> nodes;     // DFS, RtNode conventions (leaf: a = first, b = -count)
     int cap;                       // maximum depth (root = 1)
     int depth_seen = 0;
+    // SAH constants: cost of a traversal step relative to one primitive test, the largest leaf
+    // the cost rule may keep, and the size below which a node is always a leaf (defaults 1, 4, 2;
+    // RT_AMD_SAH_CT / RT_AMD_SAH_MAXLEAF / RT_AMD_SAH_FORCELEAF override, for A/B)
+    double trav_cost = env_double("RT_AMD_SAH_CT", 1.0);
+    int max_leaf = std::min(7, std::max(1, (int)env_double("RT_AMD_SAH_MAXLEAF", 4)));
+    int force_leaf = std::min(max_leaf, std::max(1, (int)env_double("RT_AMD_SAH_FORCELEAF", 2)));
+    static double env_double(const char* name, double dflt) {
+        const char* e = std::getenv(name);
+        return (e && e[0]) ? std::atof(e) : dflt;
+    }
 
     SahBuilder(const std::vector<Box>& b, int cap_) : pbox(b), cap(cap_) {
         order.resize(b.size());
@@ -1128,13 +1139,13 @@ struct SahBuilder {
             n.b = -count;
             return idx;
         };
-        if (count <= 2) return make_leaf();
+        if (count <= force_leaf) return make_leaf();
         int axis = 0;
         float ext[3] = {cb.mx.x - cb.mn.x, cb.mx.y - cb.mn.y, cb.mx.z - cb.mn.z};
         if (ext[1] > ext[axis]) axis = 1;
         if (ext[2] > ext[axis]) axis = 2;
         int mid = -1;
-        const int need = (int)std::ceil(std::log2(std::max(1.0, count / 4.0)));
+        const int need = (int)std::ceil(std::log2(std::max(1.0, count / (double)max_leaf)));
         if (ext[axis] > 0.0f && depth + need + 2 < cap) {
             constexpr int kBins = 16;
             Box binb[kBins];
@@ -1162,8 +1173,8 @@ struct SahBuilder {
                 if (c < best) { best = c; best_k = k; }
             }
             const double leaf_cost = (double)count;
-            const double split_cost = 1.0 + best / std::max(area(bb), 1e-30);
-            if (count <= 4 && !(split_cost < leaf_cost)) return make_leaf();
+            const double split_cost = trav_cost + best / std::max(area(bb), 1e-30);
+            if (count <= max_leaf && !(split_cost < leaf_cost)) return make_leaf();
             if (best_k > 0) {
                 auto it = std::partition(order.begin() + begin, order.begin() + end,
                                          [&](int32_t s) { return bin_of(pbox[(size_t)s]) < best_k; });
@@ -1172,7 +1183,7 @@ struct SahBuilder {
             }
         }
         if (mid < 0) {  // median split by centroid (balanced; also for coincident centroids)
-            if (count <= 4) return make_leaf();
+            if (count <= max_leaf) return make_leaf();
             mid = begin + count / 2;
             std::nth_element(order.begin() + begin, order.begin() + mid, order.begin() + end, [&](int32_t x, int32_t y) {
                 const float cx = cen(pbox[(size_t)x], axis), cy = cen(pbox[(size_t)y], axis);
