@@ -1047,26 +1047,43 @@ __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Re
 }
 
 // A leaf's primitives in leaf order: the fp32 pre-filter from the compact leaf-order record, then
-// the exact test (or, with DEFER, the pending-candidate rule). Trees walked from global memory
-// (S.tsph2) read one 32-byte record per primitive that also carries the fp64 radius and the slot,
-// so a sphere's exact test needs no dependent tprims -> RtPrim load (two L2 round trips).
+// the exact test (or, with DEFER, the pending-candidate rule). L2 (trees walked from global memory,
+// RT_TSPH2): one 32-byte record per primitive (S.tsph2) that also carries the fp64 radius and the
+// slot, so a sphere's exact test needs no dependent tprims -> RtPrim loads (two L2 round trips).
 // (Round 5 also tried loading a leaf's four records before its first test: spheres-100k
 // 37.1 -> 44.8 ms, spheres-500 +0 %, profiles/r05/coop_v2_prefetch/ - dropped.)
-template <class Real, bool COUNT, bool DEFER>
+#ifndef RT_TSPH2
+#define RT_TSPH2 1
+#endif
+template <class Real, bool COUNT, bool DEFER, bool L2 = false>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
                                           Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt) {
     const int v = ~ref;
     const int first = v >> 3;
     const int end = first + (v & 7);
     for (int m = first; m < end; ++m) {
-        RtLeafSph q;
-        float4 g;
-        if (!DEFER && S.tsph2) {
-            q = S.tsph2[m];
-            g = make_float4(q.c[0], q.c[1], q.c[2], q.r32);
-        } else {
-            g = S.tsph[m];
+        if constexpr (L2 && !DEFER) {
+            const RtLeafSph q = S.tsph2[m];
+            Real t;
+            bool cand;
+            if (q.r32 == q.r32) {  // sphere
+                if (COUNT) cnt[CT_SPHERE]++;
+                float lo;
+                if (!sphere_maybe(make_float4(q.c[0], q.c[1], q.c[2], q.r32), f, thi, lo)) continue;
+                if (COUNT) count_exact(cnt);
+                cand = sphere_t_cr<Real>(v3(q.c[0], q.c[1], q.c[2]), sizeof(Real) == 8 ? (Real)q.r64 : (Real)q.r32,
+                                         ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
+            } else {
+                cand = prim_candidate<Real, COUNT>(S.prims[q.slot], ray_at_use<Real>(r), f, thi, t, cnt);
+            }
+            if (cand && (t < best_t || (t == best_t && q.slot < best))) {
+                best_t = t;
+                best = q.slot;
+                thi = ::fminf(thi, upper_f<Real>(t));
+            }
+            continue;
         }
+        const float4 g = S.tsph[m];
         Real t;
         int k;  // reference leaf slot (the tie-break key)
         bool cand;
@@ -1090,17 +1107,11 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
             } else {
             if (!sphere_maybe(g, f, thi, lo)) continue;
             if (COUNT) count_exact(cnt);
-            if (S.tsph2) {
-                k = q.slot;
-                cand = sphere_t_cr<Real>(v3(q.c[0], q.c[1], q.c[2]), sizeof(Real) == 8 ? (Real)q.r64 : (Real)q.r32,
-                                         ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
-            } else {
-                k = S.tprims[m];
-                cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
-            }
+            k = S.tprims[m];
+            cand = sphere_t<Real>(S.prims[k], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t);
             }
         } else {
-            k = (!DEFER && S.tsph2) ? q.slot : S.tprims[m];
+            k = S.tprims[m];
             cand = prim_candidate<Real, COUNT>(S.prims[k], ray_at_use<Real>(r), f, thi, t, cnt);
         }
         if (cand && (t < best_t || (t == best_t && k < best))) {
@@ -1388,7 +1399,7 @@ __device__ __forceinline__ void coop_leaves(const DevScene& S, const FRay& f, co
 // Called by the whole wave with uniform control flow; lanes with `walking`
 // advance their walks. Returns when no lane walks, or (unless `drain`) after at
 // least one round once `min_ready` lanes of the wave are not walking.
-template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride>
+template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride, bool L2 = false>
 __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, bool& walking,
                                                  int* stk, int min_ready, bool drain, uint32_t* cnt, Prof* pf = nullptr) {
     const FRay f = make_fray(o, d);
@@ -1503,7 +1514,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             }
             while (leaf != kTravDone) {
                 if (PROF) pcount<PROF>(*pf, PR_LEAF);
-                leaf_test<Real, COUNT, DEFER>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
+                leaf_test<Real, COUNT, DEFER, L2>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
                 if (RT_WALK_LEAVES > 1 && leaf2 != kTravDone) {
                     leaf = leaf2;
@@ -2984,8 +2995,8 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
             psec<PROF>(pf, PR_RR);
             const bool was_walking = walking;
-            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF>(PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready,
-                                                                         exhausted, cnt, &pf);
+            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF, kStackStride, LDSS == 0 && RT_TSPH2>(
+                PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready, exhausted, cnt, &pf);
             psec<PROF>(pf, PR_HIT);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)
             if (was_walking && !walking) {

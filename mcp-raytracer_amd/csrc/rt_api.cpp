@@ -85,10 +85,7 @@ constexpr long kItemCap = (1l << 31) - (1l << 22);
 #define RT_QNODES_DEFAULT 0
 #endif
 constexpr bool kQnodesDefault = RT_QNODES_DEFAULT != 0;
-#ifndef RT_TSPH2_DEFAULT
-#define RT_TSPH2_DEFAULT 0
-#endif
-constexpr bool kTsph2Default = RT_TSPH2_DEFAULT != 0;
+
 long pass_units(long units_left, long unit_slots, long chunks_per_slot, size_t rec_bytes_per_unit, size_t budget) {
     const long by_budget = (long)(budget / std::max<size_t>(rec_bytes_per_unit, 1));
     const long by_items = (kItemCap - 1) / (std::max<long>(unit_slots, 1) * std::max<long>(chunks_per_slot, 1));
@@ -417,10 +414,11 @@ struct rt_camera {
         S.n_top = n_top;
         S.qtree = qtree ? 1 : 0;
         // trees walked from global memory: leaf records that carry the exact test's fp64 radius
-        // (RT_AMD_TSPH2=0/1 overrides)
-        S.tsph2 = g.lds_level == 0 && v.trav == TRAV_FAST && off_tsph2 >= 0 && env_flag("RT_AMD_TSPH2", kTsph2Default)
-                      ? reinterpret_cast<const RtLeafSph*>(reinterpret_cast<const char*>(d_blob) + off_tsph2)
-                      : nullptr;
+        // (the LDSS-0 chunked kernels read them, pt_kernel.hpp leaf_test L2)
+        S.tsph2 = off_tsph2 >= 0 ? reinterpret_cast<const RtLeafSph*>(reinterpret_cast<const char*>(d_blob) + off_tsph2)
+                                 : nullptr;
+        if (g.lds_level == 0 && v.trav == TRAV_FAST && !S.tsph2 && C.n_prims > 0)
+            throw std::runtime_error("fast traversal without leaf records");
         // Fixed spp: the chunked / pool kernels (per-sample records, in-order accumulate)
         // at every size. Round 1 kept the sequential kernel for images of >= 4 tiles per
         // resident wave; with the hand-out rules above the chunked kernel is faster there

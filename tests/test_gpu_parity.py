@@ -587,13 +587,13 @@ def test_large_scene_global_traversal(rt, oracle, gpu, monkeypatch):
     ro = {"width": 96, "aspect": 1, "samples": 8, "depth": 12, **NOADAPT}
     outs = []
     # (the fast walks both on the 128-byte 4-wide nodes and on the compressed 64-byte ones)
-    # and with the fp64 leaf records (tsph2) or the RtPrim loads in the exact sphere tests
-    for trav, defer, q, l2 in (("reference", "0", "0", "0"), ("fast", "0", "0", "0"), ("fast", "1", "0", "0"),
-                               ("fast", "0", "1", "0"), ("fast", "1", "1", "0"), ("fast", "0", "0", "1"),
-                               ("fast", "0", "1", "1")):
+    # (the chunked kernels read the fp64 leaf records, tsph2; the sequential kernel of the
+    # reference-order pass does not), and with SAH leaves of 2 (this size's default) and of 4
+    for trav, defer, q, leaf in (("reference", "0", "0", "2"), ("fast", "0", "0", "2"), ("fast", "1", "0", "2"),
+                                 ("fast", "0", "1", "2"), ("fast", "1", "1", "2"), ("fast", "0", "0", "4")):
         monkeypatch.setenv("RT_AMD_DEFER", defer)
         monkeypatch.setenv("RT_AMD_QNODES", q)
-        monkeypatch.setenv("RT_AMD_TSPH2", l2)
+        monkeypatch.setenv("RT_AMD_SAH_MAXLEAF", leaf)
         cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
         outs.append((rgb, rad, st))
     for k in range(1, len(outs)):
