@@ -1094,14 +1094,15 @@ struct SahBuilder {
     // the cost rule may keep, and the size below which a node is always a leaf (defaults 1, 4, 2;
     // RT_AMD_SAH_CT / RT_AMD_SAH_MAXLEAF / RT_AMD_SAH_FORCELEAF override, for A/B)
     // Trees too large for the LDS-resident copy (> kSahSmallLeafPrims primitives) are walked from
-    // global memory, where a leaf's records cost L2 round trips and its pre-filter loop runs at a
-    // fraction of the lanes: leaves of at most 2 (force 1) there - spheres-100k 2048^2 spp16
-    // 37.7 -> 35.4 ms - while LDS-resident trees keep 4 / 2 (spheres-500 with leaves of 2: 5.70 ->
-    // 7.27 ms, the larger tree no longer fits LDS) (profiles/r05/sah/).
+    // global memory, where every leaf costs an L2 round trip for its records and its pre-filter
+    // loop runs at the lanes that hold it: one primitive per leaf there (spheres-100k 2048^2 spp16,
+    // with the fp64 leaf records: leaves <= 4: 33.6 ms, <= 2: 32.1, 1: 30.1), while LDS-resident
+    // trees keep <= 4 / 2 (spheres-500 with leaves of <= 2: 5.70 -> 7.27 ms - the deeper tree and
+    // its stack no longer fit the LDS copy) (profiles/r05/sah/).
     static constexpr int kSahSmallLeafPrims = 1024;
     bool big = pbox.size() > (size_t)kSahSmallLeafPrims;
     double trav_cost = env_double("RT_AMD_SAH_CT", 1.0);
-    int max_leaf = std::min(7, std::max(1, (int)env_double("RT_AMD_SAH_MAXLEAF", big ? 2 : 4)));
+    int max_leaf = std::min(7, std::max(1, (int)env_double("RT_AMD_SAH_MAXLEAF", big ? 1 : 4)));
     int force_leaf = std::min(max_leaf, std::max(1, (int)env_double("RT_AMD_SAH_FORCELEAF", big ? 1 : 2)));
     static double env_double(const char* name, double dflt) {
         const char* e = std::getenv(name);

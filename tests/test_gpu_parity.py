@@ -588,9 +588,10 @@ def test_large_scene_global_traversal(rt, oracle, gpu, monkeypatch):
     outs = []
     # (the fast walks both on the 128-byte 4-wide nodes and on the compressed 64-byte ones)
     # (the chunked kernels read the fp64 leaf records, tsph2; the sequential kernel of the
-    # reference-order pass does not), and with SAH leaves of 2 (this size's default) and of 4
-    for trav, defer, q, leaf in (("reference", "0", "0", "2"), ("fast", "0", "0", "2"), ("fast", "1", "0", "2"),
-                                 ("fast", "0", "1", "2"), ("fast", "1", "1", "2"), ("fast", "0", "0", "4")):
+    # reference-order pass does not), and with SAH leaves of 1 (this size's default), 2 and 4
+    for trav, defer, q, leaf in (("reference", "0", "0", "1"), ("fast", "0", "0", "1"), ("fast", "1", "0", "1"),
+                                 ("fast", "0", "1", "1"), ("fast", "1", "1", "1"), ("fast", "0", "0", "2"),
+                                 ("fast", "0", "0", "4")):
         monkeypatch.setenv("RT_AMD_DEFER", defer)
         monkeypatch.setenv("RT_AMD_QNODES", q)
         monkeypatch.setenv("RT_AMD_SAH_MAXLEAF", leaf)
