@@ -1055,19 +1055,17 @@ __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Re
 #ifndef RT_TSPH2
 #define RT_TSPH2 1
 #endif
-#ifndef RT_LEAF_PRE
-#define RT_LEAF_PRE 0  // L2 walks: load a parked leaf's first record when it is parked (A/B)
-#endif
+// (Also tried: loading a parked leaf's record when it is parked, so the load overlaps the rest of
+// the node loop - spheres-100k 30.0 -> 36.0 ms, profiles/r05/leaf_pre/.)
 template <class Real, bool COUNT, bool DEFER, bool L2 = false>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
-                                          Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt,
-                                          const RtLeafSph* pre = nullptr) {
+                                          Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt) {
     const int v = ~ref;
     const int first = v >> 3;
     const int end = first + (v & 7);
     for (int m = first; m < end; ++m) {
         if constexpr (L2 && !DEFER) {
-            const RtLeafSph q = (pre && m == first) ? *pre : S.tsph2[m];
+            const RtLeafSph q = S.tsph2[m];
             Real t;
             bool cand;
             if (q.r32 == q.r32) {  // sphere
@@ -1499,18 +1497,11 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             // one round of closest_hit_fast's parked-leaf walk (RT_WALK_LEAVES = 2: a lane
             // parks a second leaf and keeps stepping instead of idling until the leaf phase)
             int ref = W.ref, leaf = W.leaf, leaf2 = kTravDone;
-            constexpr bool PRE = L2 && !DEFER && RT_LEAF_PRE;
-            RtLeafSph pre;  // PRE: the parked leaf's first record, loaded while the walk goes on
-            bool have_pre = false;
             while (ref >= 0) {
                 if (PROF) pcount<PROF>(*pf, PR_NODE);
                 ref = node_step(ref);
                 if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
                     leaf = ref;
-                    if constexpr (PRE) {
-                        pre = S.tsph2[(~ref) >> 3];
-                        have_pre = true;
-                    }
                     ref = pop();
                 } else if (RT_WALK_LEAVES > 1 && ref < 0 && ref != kTravDone && leaf2 == kTravDone) {
                     leaf2 = ref;
@@ -1525,9 +1516,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
             }
             while (leaf != kTravDone) {
                 if (PROF) pcount<PROF>(*pf, PR_LEAF);
-                leaf_test<Real, COUNT, DEFER, L2>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt,
-                                                  PRE && have_pre ? &pre : nullptr);
-                have_pre = false;
+                leaf_test<Real, COUNT, DEFER, L2>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
                 if (RT_WALK_LEAVES > 1 && leaf2 != kTravDone) {
                     leaf = leaf2;
