@@ -69,12 +69,15 @@ hipError_t launch_tiles_unpack(const void* slabs, int groups, int slab_tiles, co
 
 // LDS bytes per workgroup for the traversal stack (fast / reference) or the
 // per-lane candidate bounds of the nearest-first brute force.
-inline size_t stack_lds_bytes(int stack_depth, int trav, int n_prims) {
+// `lds_tree`: the launch's tree is LDS-resident (LDSS > 0), whose fast-walk stack entries are 16-bit
+// (StackT, pt_kernel.hpp)
+inline size_t stack_lds_bytes(int stack_depth, int trav, int n_prims, bool lds_tree = false) {
     if (trav == TRAV_BRUTE)  // larger forced brute-force scenes take the in-order loop (no LDS)
         return RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims ? (size_t)std::max(n_prims, 1) * kStackStride * sizeof(uint16_t)
                                                            : 0;
     const size_t d = (size_t)(stack_depth > 0 ? stack_depth : 1);
-    return d * kStackStride * ((trav == TRAV_FAST && kStackTnear) ? 2 * sizeof(int) : sizeof(int));
+    const size_t e = lds_tree ? sizeof(StackT<1>) : sizeof(StackT<0>);
+    return d * kStackStride * ((trav == TRAV_FAST && kStackTnear) ? 2 * e : e);
 }
 
 // The kernel template instance of a launch (one per scalar precision unit: pt_ref.hip,

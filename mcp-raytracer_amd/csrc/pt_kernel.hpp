@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "rt_math.hpp"
 #include "scene.hpp"
@@ -155,6 +156,15 @@ constexpr int kWave = 64;
 constexpr int kBlock = RT_SEQ_BLOCK;
 constexpr int kBlockChunk = RT_CHUNK_BLOCK;
 constexpr int kStackStride = 1024;  // LDS traversal-stack column stride (>= any block size)
+// Stack entries of the fast walk (RT_STK16): 16-bit in launches whose tree is LDS-resident (its
+// node references and leaf codes ~(first << 3 | count) fit an int16: at most ~1,000 nodes and
+// primitives fit the LDS copy), so the stack takes half the LDS and the material / light tables
+// fit beside it (LDS residency level 2); 32-bit where the tree is walked from global memory.
+#ifndef RT_STK16
+#define RT_STK16 1
+#endif
+template <int LDSS>
+using StackT = typename std::conditional<(LDSS > 0 && RT_STK16 != 0), int16_t, int32_t>::type;
 // Fast traversal stack entries: node reference only (4 B; a popped subtree is
 // culled one level later by its children's slab tests), or also its entry
 // distance (8 B; culled on pop). 4 B keeps deeper SAH trees LDS-resident.
@@ -547,8 +557,8 @@ __device__ __forceinline__ bool prim_t(const RtPrim& p, const RayK<Real>& r, Rea
 // box is tested when a node is entered with the closest-so-far interval, left
 // subtree before right, leaf primitives in leaf order with a narrowing max.
 // `stk` points at this lane's column of the LDS stack (stride kStackStride ints).
-template <class Real, bool COUNT>
-__device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
+template <class Real, bool COUNT, class SK>
+__device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& r, Real& t_hit, SK* stk,
                                            uint32_t* cnt) {
     const Real tmin = K<Real>::TMIN;
     Real tmax = (Real)__builtin_inf();
@@ -570,7 +580,7 @@ __device__ __forceinline__ int closest_hit(const DevScene& S, const RayK<Real>& 
                     }
                 }
             } else {
-                stk[sp * kStackStride] = nd.b;
+                stk[sp * kStackStride] = (SK)nd.b;
                 ++sp;
                 node = nd.a;
                 descend = true;
@@ -756,8 +766,8 @@ __device__ __forceinline__ void t4_rows(const void* nd0, const FRay& f, bool nf,
 //    (scene.cpp: stack_depth = max(..., 3 t4depth + 1) + 1).
 // The pair sort and stack pushes of a 4-wide node step (below): keys k (entry-distance bits, ~0
 // for a miss), child references r, n hit children.
-template <int STRIDE>
-__device__ __forceinline__ int t4_push(uint32_t (&k)[4], int (&r)[4], int n, int* stk, int& sp) {
+template <int STRIDE, class SK>
+__device__ __forceinline__ int t4_push(uint32_t (&k)[4], int (&r)[4], int n, SK* stk, int& sp) {
     auto cx = [&](int i, int j) {
         const bool sw = k[j] < k[i];
         const uint32_t lo = min(k[i], k[j]), hi = max(k[i], k[j]);
@@ -770,7 +780,7 @@ __device__ __forceinline__ int t4_push(uint32_t (&k)[4], int (&r)[4], int n, int
     cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
     const int popped = stk[max(sp - 1, 0) * STRIDE];
 #pragma unroll
-    for (int j = 3; j >= 1; --j) stk[max(sp + n - 1 - j, sp) * STRIDE] = r[j];
+    for (int j = 3; j >= 1; --j) stk[max(sp + n - 1 - j, sp) * STRIDE] = (SK)r[j];
     const int next = n > 0 ? r[0] : (sp > 0 ? popped : kT4Empty);  // (kT4Empty = kTravDone)
     sp = n > 0 ? sp + n - 1 : max(sp - 1, 0);
     return next;
@@ -783,8 +793,8 @@ __device__ __forceinline__ int t4_push(uint32_t (&k)[4], int (&r)[4], int n, int
 // bytes per node: 4 row loads instead of 7, and twice the nodes in the LDS top cache (80-byte
 // stride there: 20 i + 4 r covers 16 bank windows for i mod 16).
 constexpr int kQ4LdsStride = (int)sizeof(RtQ4Node) + 16;
-template <int STRIDE>
-__device__ __forceinline__ int q4_step(const DevScene& S, int ref, const FRay& f, float thi, int* stk, int& sp) {
+template <int STRIDE, class SK>
+__device__ __forceinline__ int q4_step(const DevScene& S, int ref, const FRay& f, float thi, SK* stk, int& sp) {
     typedef float v4 __attribute__((ext_vector_type(4)));
     v4 h0, h1, h2, h3;
     if (ref < S.n_top) {
@@ -824,8 +834,8 @@ __device__ __forceinline__ int q4_step(const DevScene& S, int ref, const FRay& f
     return t4_push<STRIDE>(k, r, n, stk, sp);
 }
 
-template <int STRIDE>
-__device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f, float thi, int* stk, int& sp) {
+template <int STRIDE, class SK>
+__device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f, float thi, SK* stk, int& sp) {
     if (S.qtree) return q4_step<STRIDE>(S, ref, f, thi, stk, sp);
     T4Rows R;
     const bool nf = RT_NEARFAR && S.nearfar;
@@ -1124,8 +1134,8 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
     }
 }
 
-template <class Real, bool COUNT, bool DEFER>
-__device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Real>& r, Real& t_hit, int* stk,
+template <class Real, bool COUNT, bool DEFER, class SK>
+__device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Real>& r, Real& t_hit, SK* stk,
                                                 float* stkt, uint32_t* cnt) {
     const FRay f = make_fray(r.o, r.d);
     Real best_t = (Real)__builtin_inf();
@@ -1165,7 +1175,7 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
         const bool hb = slab(nd.box[1], f, thi, tb);
         if (ha && hb) {
             const bool a_first = ta <= tb;
-            stk[sp * kStackStride] = a_first ? nd.box[1].a : nd.box[0].a;
+            stk[sp * kStackStride] = (SK)(a_first ? nd.box[1].a : nd.box[0].a);
             if (kStackTnear) stkt[sp * kStackStride] = a_first ? tb : ta;
             ++sp;
             return a_first ? nd.box[0].a : nd.box[1].a;
@@ -1401,9 +1411,10 @@ __device__ __forceinline__ void coop_leaves(const DevScene& S, const FRay& f, co
 // Called by the whole wave with uniform control flow; lanes with `walking`
 // advance their walks. Returns when no lane walks, or (unless `drain`) after at
 // least one round once `min_ready` lanes of the wave are not walking.
-template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride, bool L2 = false>
+template <class Real, bool COUNT, bool DEFER, bool PROF = false, int STRIDE = kStackStride, bool L2 = false,
+          class SK = int>
 __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, FastWalk<Real>& W, bool& walking,
-                                                 int* stk, int min_ready, bool drain, uint32_t* cnt, Prof* pf = nullptr) {
+                                                 SK* stk, int min_ready, bool drain, uint32_t* cnt, Prof* pf = nullptr) {
     const FRay f = make_fray(o, d);
     const RayK<Real> r = make_ray<Real>(o, d);
     float* stkt = nullptr;
@@ -1486,7 +1497,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 const bool hb = slab(nd.box[1], f, thi, tb);
                 if (ha && hb) {
                     const bool a_first = ta <= tb;
-                    stk[sp * STRIDE] = a_first ? nd.box[1].a : nd.box[0].a;
+                    stk[sp * STRIDE] = (SK)(a_first ? nd.box[1].a : nd.box[0].a);
                     ++sp;
                     return a_first ? nd.box[0].a : nd.box[1].a;
                 }
@@ -1743,7 +1754,8 @@ __device__ __forceinline__ uint16_t lot_store(float lo) {
 }
 __device__ __forceinline__ float lot_load(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 // This lane's fp16 column base (stk = the block's LDS base + threadIdx.x, as int*).
-__device__ __forceinline__ uint16_t* lot_column(int* stk) {
+template <class SK>
+__device__ __forceinline__ uint16_t* lot_column(SK* stk) {
     return reinterpret_cast<uint16_t*>(stk - threadIdx.x) + threadIdx.x;
 }
 
@@ -2057,8 +2069,8 @@ __device__ __forceinline__ const RtCamera& cam_opaque() {
     return *(const RtCamera*)(p + offsetof(DevScene, cam));  // addrspacecast; inferred back to constant
 }
 
-template <class Real, bool COUNT, int TRAV>
-__device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t, int* stk,
+template <class Real, bool COUNT, int TRAV, class SK>
+__device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t, SK* stk,
                                                float* stkt, uint32_t* cnt) {
     if (TRAV == TRAV_BRUTE) {
         if (RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims)
@@ -2366,8 +2378,8 @@ __device__ __forceinline__ bool path_post(const DevScene& S, const RtCamera& C, 
 // One level of rayColor (src/camera.ts:221-319): path_pre, the closest hit,
 // path_post. Returns true when the path ends; `c` is then the sample's radiance
 // (the recursion's emitted + ... right fold included).
-template <class Real, bool EMIT, bool COUNT, bool PROF, int TRAV>
-__device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, Path<EMIT>& P, int* stk, float* stkt,
+template <class Real, bool EMIT, bool COUNT, bool PROF, int TRAV, class SK>
+__device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, Path<EMIT>& P, SK* stk, float* stkt,
                                           uint32_t* cnt, unsigned long long& st_err, Prof& pf, V3& c) {
     if (path_pre<Real, EMIT, PROF>(C, P, pf, c)) return true;
     const RayK<Real> ray = make_ray<Real>(P.o, P.d);
@@ -2552,7 +2564,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
     const RtCamera& C = S0.cam;
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
-    int* stk = lds_stack + threadIdx.x;
+    StackT<LDSS>* stk = reinterpret_cast<StackT<LDSS>*>(lds_stack) + threadIdx.x;
     float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C.stack_depth * kStackStride + threadIdx.x;
 
     const int endX = min(reg.x + reg.width, C.width);
@@ -2889,7 +2901,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     phase_table_init(sb, ptab);
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
-    int* stk = lds_stack + threadIdx.x;
+    StackT<LDSS>* stk = reinterpret_cast<StackT<LDSS>*>(lds_stack) + threadIdx.x;
     float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kStackStride + threadIdx.x;
     const int endX = min(reg.x + reg.width, C0.width);
     const int endY = min(reg.y + reg.height, C0.height);
@@ -3189,7 +3201,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     phase_table_init(sb, ptab);
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
-    int* stk = lds_stack + threadIdx.x;
+    StackT<LDSS>* stk = reinterpret_cast<StackT<LDSS>*>(lds_stack) + threadIdx.x;
     float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kStackStride + threadIdx.x;
     char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * kPoolWaveBytes;
     float4* G = reinterpret_cast<float4*>(wpool);  // group q of slot k: G[q * kPoolK + k]

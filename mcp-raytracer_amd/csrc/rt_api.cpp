@@ -355,7 +355,8 @@ struct rt_camera {
         const long want = (mine + (kBlock / kWave) - 1) / (kBlock / kWave);
         g.grid = (int)std::max<long>(1, std::min<long>(want, (long)cus));  // one persistent workgroup per CU
         KernelVariant v{C.emissive_scatter != 0, count, effective_traversal(trav)};
-        const size_t stack = stack_lds_bytes(C.stack_depth, v.trav, C.n_prims);
+        const size_t stack0 = stack_lds_bytes(C.stack_depth, v.trav, C.n_prims);        // tree in global memory
+        const size_t stack1 = stack_lds_bytes(C.stack_depth, v.trav, C.n_prims, true);  // LDS-resident tree
         // LDS-resident scene: the BVH walk's data and the primitive records
         // (level 1), plus the material and light tables when they fit too
         // (level 2). The brute-force loop reads its wave-uniform primitive
@@ -367,11 +368,17 @@ struct rt_camera {
             RT_BVH4 && v.trav == TRAV_FAST && env_flag("RT_AMD_NODE_PAD", true) ? (int32_t)build.t4nodes.size() : 0;
         g.lds_level = 0;
         if (lds_scene_enabled() && v.trav != TRAV_REFERENCE) {
-            if (stack + (size_t)(lds_words2 + node_pad) * 16 <= lds_cap && env_flag("RT_AMD_LDS_MATS", true))
+            if (stack1 + (size_t)(lds_words2 + node_pad) * 16 <= lds_cap && env_flag("RT_AMD_LDS_MATS", true))
                 g.lds_level = 2;
-            else if (v.trav == TRAV_FAST && stack + (size_t)(lds_words + node_pad) * 16 <= lds_cap)
+            else if (v.trav == TRAV_FAST && stack1 + (size_t)(lds_words + node_pad) * 16 <= lds_cap)
                 g.lds_level = 1;
         }
+        // (16-bit stack entries hold node references < 2^15 and leaf codes ~(first << 3 | count) with
+        // first < 2^12: always so for a tree that fits the LDS copy; checked)
+        if (g.lds_level > 0 && v.trav == TRAV_FAST && RT_STK16 &&
+            (build.t4nodes.size() >= (1u << 15) || build.tprims.size() >= (1u << 12)))
+            g.lds_level = 0;
+        const size_t stack = g.lds_level > 0 ? stack1 : stack0;
         g.lds_bytes = stack + (g.lds_level == 0 ? 0 : (size_t)((g.lds_level == 2 ? lds_words2 : lds_words) + node_pad) * 16);
         // a tree walked from global memory: its top (breadth-first prefix) in the LDS left beside the stack
         int32_t n_top = 0;
