@@ -1093,17 +1093,18 @@ struct SahBuilder {
     // SAH constants: cost of a traversal step relative to one primitive test, the largest leaf
     // the cost rule may keep, and the size below which a node is always a leaf (defaults 1, 4, 2;
     // RT_AMD_SAH_CT / RT_AMD_SAH_MAXLEAF / RT_AMD_SAH_FORCELEAF override, for A/B)
-    // Trees too large for the LDS-resident copy (> kSahSmallLeafPrims primitives) are walked from
-    // global memory, where every leaf costs an L2 round trip for its records and its pre-filter
-    // loop runs at the lanes that hold it: one primitive per leaf there (spheres-100k 2048^2 spp16,
-    // with the fp64 leaf records: leaves <= 4: 33.6 ms, <= 2: 32.1, 1: 30.1), while LDS-resident
-    // trees keep <= 4 / 2 (spheres-500 with leaves of <= 2: 5.70 -> 7.27 ms - the deeper tree and
-    // its stack no longer fit the LDS copy) (profiles/r05/sah/).
-    static constexpr int kSahSmallLeafPrims = 1024;
-    bool big = pbox.size() > (size_t)kSahSmallLeafPrims;
+    // One primitive per leaf where the walk tests a leaf's primitives exactly as it reaches them
+    // (no deferred exact tests, pt_kernel.hpp leaf_test): trees too large for the LDS-resident copy
+    // (> 1,024 primitives: every leaf costs an L2 round trip for its records and its pre-filter loop
+    // runs at the lanes that hold it; spheres-100k 2048^2 spp16 with the fp64 leaf records: leaves
+    // <= 4: 33.6 ms, <= 2: 32.1, 1: 30.1) and small ones (< 100 primitives; rain-50 1080p spp128:
+    // 11.09 -> 10.91 ms). LDS-resident trees of 100 .. 1,024 primitives run the deferred exact tests
+    // (rt_api.cpp v.defer), whose leaf loop is cheap per primitive: they keep <= 4 / 2 (spheres-500:
+    // leaves of 1 5.72 -> 5.76 ms, of <= 2 7.27 ms) (profiles/r05/sah/).
+    bool one_leaf = pbox.size() > 1024 || pbox.size() < 100;
     double trav_cost = env_double("RT_AMD_SAH_CT", 1.0);
-    int max_leaf = std::min(7, std::max(1, (int)env_double("RT_AMD_SAH_MAXLEAF", big ? 1 : 4)));
-    int force_leaf = std::min(max_leaf, std::max(1, (int)env_double("RT_AMD_SAH_FORCELEAF", big ? 1 : 2)));
+    int max_leaf = std::min(7, std::max(1, (int)env_double("RT_AMD_SAH_MAXLEAF", one_leaf ? 1 : 4)));
+    int force_leaf = std::min(max_leaf, std::max(1, (int)env_double("RT_AMD_SAH_FORCELEAF", one_leaf ? 1 : 2)));
     static double env_double(const char* name, double dflt) {
         const char* e = std::getenv(name);
         return (e && e[0]) ? std::atof(e) : dflt;
