@@ -8,9 +8,11 @@ times each group; an N-GPU step lasts as long as the SLOWEST rank, so the projec
     T(N) = max_g share(g) + gather(N slabs) + unpack(N slabs)
 
 where `gather` is measured as N real `dist.gather` calls of one slab each over a world-size-1
-"nccl" (= RCCL) group (RCCL refuses two ranks on one device; on the 8-GPU node the N - 1 remote
-slabs arrive over separate xGMI links, so this local-copy figure is a lower bound - each slab is
-frame / N bytes, 1.92 MB / N for Cornell, ~13 us per 1.9 MB at 150 GB/s) and `unpack` is
+"nccl" (= RCCL) group (RCCL refuses two ranks on one device). On the 8-GPU node the gather is ONE
+call whose N - 1 remote slabs (frame / N bytes each: 240 KB for an 800^2 frame at N = 8, ~2 us on
+one 150 GB/s xGMI link) arrive in parallel, so the N sequential calls - dominated by per-call
+overhead - bound it from above; one world-1 collective over all N slabs is reported beside it
+(`gather_one_call_ms`, `efficiency_one_call_gather`). `unpack` is
 rt_tiles_unpack of the gathered [N, slab, 3] buffer into the frame. The reference's counterpart:
 worker row bands, src/raytracer.ts:60-90,185-205. Prints one JSON line per N with the max / min
 / mean share, the projected step and its efficiency T(1) / (N T(N)).
@@ -76,6 +78,11 @@ def run(scene, reps):
             for g in range(n):
                 dist.gather(slabs[g], gather_list=[gathered[g]], dst=0)
         t_gather = _timed(gather, reps)
+        # one collective moving all N slabs (the real N-rank gather is ONE call: N - 1 slabs arrive
+        # at rank 0 at once over separate xGMI links); the N sequential calls above bound it above
+        flat = slabs.reshape(-1)
+        flat_out = torch.empty_like(flat)
+        t_gather1 = _timed(lambda: dist.all_gather_into_tensor(flat_out, flat), reps)
         t_unpack = _timed(lambda: rtd.unpack_tiles(gathered, region, W, H, frame, s, slab_tiles=n_tiles + 1), reps)
         # the assembled frame must be the single launch's (the rehearsal renders the real shares)
         single = torch.zeros_like(frame)
@@ -87,8 +94,10 @@ def run(scene, reps):
                                                "mean": round(sum(shares) / n, 3),
                                                "slowest_group": shares.index(max(shares))},
             "path_kernel_ms_max": round(max(k[0] for k in kernels), 3),
-            "gather_world1_ms": round(t_gather, 4), "unpack_ms": round(t_unpack, 4),
+            "gather_world1_ms": round(t_gather, 4), "gather_one_call_ms": round(t_gather1, 4),
+            "unpack_ms": round(t_unpack, 4),
             "projected_step_ms": round(proj, 3), "efficiency": round(t1 / (n * proj), 4),
+            "efficiency_one_call_gather": round(t1 / (n * (max(shares) + t_gather1 + t_unpack)), 4),
             "efficiency_share_only": round(t1 / (n * max(shares)), 4), "frame_equals_single": ok}), flush=True)
         if not ok:
             raise SystemExit(f"{scene} N={n}: assembled frame differs from the single launch")
