@@ -2721,14 +2721,22 @@ __device__ __forceinline__ void rec_store(float4* p, float4 r);
 // a 12-byte record (loads / stores of a 3-element vector move 12 bytes; its sizeof is 16, so
 // records are addressed in floats)
 typedef float RecF3 __attribute__((ext_vector_type(3), aligned(4)));
-// A lane's bounce statistics over the samples it recorded (SampleBuf::rec12)
-// (sum in 64 bits: a lane records ~10^4 samples per launch at the 8 GB record budget and depth
-// goes up to 1e9, so a 32-bit sum could wrap - ADVICE r04)
+// A lane's bounce statistics over the samples it recorded (SampleBuf::rec12). The sum is 32-bit
+// with a carry: a lane records ~10^4 samples per launch at the 8 GB record budget and depth goes
+// up to 1e9, so a 32-bit sum can wrap; on a wrap the old sum goes to the launch's
+// bounce total by one atomic (never in practice: 2^32 bounces in one lane's launch). (A 64-bit
+// sum instead cost the pool kernel an extra spilled register reloaded in its trip loop: Cornell
+// 13.91 -> 14.02 ms, profiles/r05/final/.)
 struct LaneBounces {
-    unsigned long long sum = 0;
-    uint32_t mn = 0xffffffffu, mx = 0;
-    __device__ void add(int b) {
-        sum += (unsigned long long)(uint32_t)b;
+    uint32_t sum = 0, mn = 0xffffffffu, mx = 0;
+    __device__ void add(int b, unsigned long long* stats) {
+        const uint32_t ns = sum + (uint32_t)b;
+        if (ns < sum) {
+            atomicAdd(stats + ST_BOUNCES * kStatStride, (unsigned long long)sum);
+            sum = (uint32_t)b;
+        } else {
+            sum = ns;
+        }
         mn = min(mn, (uint32_t)b);
         mx = max(mx, (uint32_t)b);
     }
@@ -2742,12 +2750,13 @@ struct LaneBounces {
 // The sample's record at index `idx` (s * stride_s + slot * stride_slot): {rgb, w} or, with
 // rec12, {rgb} and w's bounce count into the lane's statistics.
 template <bool NT>
-__device__ __forceinline__ void rec_put(const SampleBuf& sb, size_t idx, V3 c, int w, LaneBounces& lb) {
+__device__ __forceinline__ void rec_put(const SampleBuf& sb, size_t idx, V3 c, int w, LaneBounces& lb,
+                                        unsigned long long* stats) {
     if (sb.rec12) {
         RecF3* p = reinterpret_cast<RecF3*>(reinterpret_cast<float*>(sb.rec) + 3 * idx);
         if constexpr (NT) __builtin_nontemporal_store(RecF3{c.x, c.y, c.z}, p);
         else *p = RecF3{c.x, c.y, c.z};
-        lb.add(w);
+        lb.add(w, stats);
     } else {
         rec_store<NT>(sb.rec + idx, make_float4(c.x, c.y, c.z, __int_as_float(w)));
     }
@@ -2984,7 +2993,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             // the sample's radiance and bounce count to its record; next sample or idle
             auto finish_sample = [&](V3 c) {
                 rec_put<false>(PK_SB, (size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot, c,
-                               P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err), lb);
+                               P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err), lb, PK_OUT.stats);
                 ++s;
                 if (s < s_end) new_path = true;
                 else slot = -1;
@@ -3077,7 +3086,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(PK_S, C, P, stk, stkt, cnt, st_err, pf, c)) {
 #ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
                 rec_put<false>(PK_SB, (size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot, c,
-                               P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err), lb);
+                               P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err), lb, PK_OUT.stats);
 #endif
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;
@@ -3239,7 +3248,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     auto record = [&](V3 c, int bounces, int slot, int& s, int s_end, unsigned long long err = 0ull) -> int {
         if (!sb.err_in_rec) st_err |= err;
         rec_put<RT_REC_NT>(sb, (size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot, c,
-                           bounces | (sb.err_in_rec ? (int)((uint32_t)err << kRecErrShift) : 0), lb);
+                           bounces | (sb.err_in_rec ? (int)((uint32_t)err << kRecErrShift) : 0), lb, out.stats);
         ++s;
         return s < s_end ? PH_NEW : PH_ITEM;
     };
