@@ -43,10 +43,10 @@ CLASSES = [
 ]
 
 
-def compile_unit(unit: str, out: Path, defines) -> Path:
+def compile_unit(unit: str, out: Path, defines, extra=()) -> Path:
     out.mkdir(parents=True, exist_ok=True)
     flags = dict((u[0], u[1]) for u in _build._UNITS)[unit]
-    cmd = [_build.hipcc(), *_build._COMMON, *flags, *[f"-D{d}" for d in defines], '-DRT_BUILD_ID="isa"',
+    cmd = [_build.hipcc(), *_build._COMMON, *flags, *[f"-D{d}" for d in defines], *extra, '-DRT_BUILD_ID="isa"',
            f"--offload-arch={_build.ARCH}", "--offload-device-only", "-save-temps", "-c",
            str(_build.CSRC / unit), "-o", str(out / "unit.o")]
     subprocess.run(cmd, check=True, cwd=out)
@@ -105,12 +105,13 @@ def main():
     ap.add_argument("--unit", default="pt_ref.hip")
     ap.add_argument("--out", default="/tmp/isa")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--flag", dest="flags", action="append", default=[], help="extra compiler flag (repeatable)")
     ap.add_argument("--reuse", action="store_true", help="parse the assembly already in --out")
     a = ap.parse_args()
     if a.reuse:
         s_path = sorted(Path(a.out).glob("*gfx950*.s"))[0]
     else:
-        s_path = compile_unit(a.unit, Path(a.out), a.defines)
+        s_path = compile_unit(a.unit, Path(a.out), a.defines, a.flags)
     asm = s_path.read_text()
     demangled = {}
     syms = [sym for sym, _ in functions(asm)]
@@ -123,10 +124,11 @@ def main():
         if not any(re.search(p, name) for p in a.patterns):
             continue
         c = stats(body)
+        c["scratch"] = sum(1 for line in body if line.strip().startswith("scratch_"))
         md = meta(asm, sym)
         print(name)
         print("  regs:", md)
-        print("  " + " ".join(f"{k}={c[k]}" for k in ["total"] + [n for n, _ in CLASSES] if c[k]))
+        print("  " + " ".join(f"{k}={c[k]}" for k in ["total"] + [n for n, _ in CLASSES] + ["scratch"] if c[k]))
 
 
 if __name__ == "__main__":
