@@ -34,7 +34,15 @@ _COMMON = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-
 # from 128 VGPRs + 8 spilled (scratch reloads inside the pre-filter loop) to
 # 111 VGPRs and no spills: Cornell 7071 -> 7647, spheres-500 4878 -> 5096,
 # rain 19821 -> 20212 Msamples/s (profiles/r01/noslp/).
-_KERNEL_FLAGS = ["-fno-slp-vectorize"]
+# -disable-machine-licm on the kernel units (round 5): the machine-code loop-invariant motion
+# hoisted the fp64 polynomial constants of ocml's sincos (and a few other constants) out of the
+# path loops into VGPR pairs it then spilled to scratch, reloading them after every cosine-PDF
+# sincos: 84-104 B of scratch per lane in the BVH chunk kernels, 40 B in the pool kernel, all
+# at the 128-VGPR cap. Without it the constants are rematerialised where they are used: no
+# scratch, 97-126 VGPRs; Cornell 13.97 -> 13.72 ms, spheres-500 5.70 -> 5.64, rain spp128
+# 10.97 -> 10.82, spheres-100k 2048^2 spp16 30.06 -> 29.15 ms path kernel, bit-exact
+# (profiles/r05/nolicm/).
+_KERNEL_FLAGS = ["-fno-slp-vectorize", "-mllvm", "-disable-machine-licm"]
 _UNITS = [
     ("pt_ref.hip", ["-ffp-contract=off", *_KERNEL_FLAGS], True),
     ("pt_fp32.hip", ["-ffp-contract=fast", *_KERNEL_FLAGS], True),
