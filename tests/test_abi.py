@@ -31,6 +31,29 @@ def test_library_is_gfx950_code_object(rt):
     assert b"pt_render_kernel" in data
 
 
+def test_product_kernels_do_not_spill_to_scratch(rt):
+    """Every kernel a product render launches keeps its state in registers: a scratch reload
+    inside the path loop misses L2 behind the record stream (round 5: the fp64 sincos constants
+    MachineLICM hoisted and spilled cost 1-3 % and doubled the record write traffic; DESIGN.md
+    §4). Instrumented (INSTR > 0) and emission-stack (EMIT) variants are diagnostic or keep the
+    stack in scratch by design."""
+    import sys
+    from pathlib import Path
+    from raytracer_amd import _lib
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import kernel_resources
+    ks = kernel_resources.resources(_lib.LIB_PATH)
+    assert len(ks) > 40
+    # pt_pool_kernel<Real, TRAV, LDSS>; pt_chunk_kernel / pt_render_kernel<Real, EMIT=false, INSTR=0, ...>
+    product = re.compile(r"pt_pool_kernel|pt_(chunk|render)_kernelI[df]Lb0ELi0E|pt_accum_kernel|pt_adapt_kernel")
+    checked = [k for k in ks if product.search(k["name"])]
+    assert len(checked) >= 20
+    spills = [(k["name"], k["scratch"]) for k in checked if k["scratch"] != 0]
+    assert not spills, spills
+    # the persistent 1024-thread workgroups run 4 waves per SIMD: <= 128 VGPRs
+    assert max(k["vgpr"] for k in checked if re.search(r"pt_(pool|chunk)_kernel", k["name"])) <= 128
+
+
 def test_camera_info_defaults_and_merge_order(rt):
     sd = rt.generate_scene_data({"type": "cornell"})
     cam = rt.create_camera_from_scene_data(sd)  # render defaults + scene render {aspect 1, rouletteDepth 5}
