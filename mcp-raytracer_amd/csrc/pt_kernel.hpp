@@ -2845,6 +2845,45 @@ __device__ __forceinline__ void item_decode(const SampleBuf& sb, const PhaseRow*
     s_end = s + r.chunk;
 }
 
+// Diagnostic (RT_WAVE_PROBE=1 variant builds only): per wave of a chunked / pool launch, the
+// real-time clock (100 MHz) at its start, when the hand-out ran dry for it and at its end, the
+// items it took and its hardware ids - where a launch's tail goes (tools/wave_probe.py).
+#ifndef RT_WAVE_PROBE
+#define RT_WAVE_PROBE 0
+#endif
+constexpr int kWaveProbeSlots = 8192;  // waves (256 CUs x 16 waves, twice over)
+#if RT_WAVE_PROBE
+static __device__ unsigned long long g_wave_probe[kWaveProbeSlots * 4];
+struct WaveProbe {
+    unsigned long long t0 = 0, tx = 0;
+    unsigned int items = 0;
+    __device__ void start() { t0 = __builtin_amdgcn_s_memrealtime(); }
+    __device__ void took(int n, bool exhausted) {
+        items += (unsigned int)n;
+        if (exhausted && tx == 0) tx = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ void finish(int lane, int waves_per_block) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const int w = blockIdx.x * waves_per_block + (int)(threadIdx.x / kWave);
+        const unsigned int hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        const unsigned int xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20); // XCC_ID
+        if (lane == 0 && w < kWaveProbeSlots) {
+            g_wave_probe[4 * w + 0] = t0;
+            g_wave_probe[4 * w + 1] = tx ? tx : t1;
+            g_wave_probe[4 * w + 2] = t1;
+            g_wave_probe[4 * w + 3] = ((unsigned long long)items << 32) | ((unsigned long long)(xcc & 0xf) << 28) |
+                                      (hw & 0x0fffffffu);
+        }
+    }
+};
+#else
+struct WaveProbe {
+    __device__ void start() {}
+    __device__ void took(int, bool) {}
+    __device__ void finish(int, int) {}
+};
+#endif
+
 // Item hand-out: every wave's first pool is static (wave w takes items
 // [w * pool, (w + 1) * pool)), the global counter deals the rest from
 // grid_waves * pool on - so the launch does not open with every wave's atomic
@@ -2926,6 +2965,8 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     Prof pf;
     prof_init<PROF>(pf, prof_lds, lane);
 
+    WaveProbe wprobe;
+    wprobe.start();
     int pool_next, pool_end;  // wave-uniform
     bool exhausted;           // wave-uniform
     first_pool(sb, pool_next, pool_end, exhausted);
@@ -2965,6 +3006,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
         const int n_need = __popcll(need);
         if (n_need != 0 && !exhausted && (n_need >= PK_SB.refill_min || __ballot(slot >= 0) == 0ull)) {
             if (pool_next >= pool_end) take_pool(PK_OUT, PK_SB, lane, pool_next, pool_end, exhausted);
+            wprobe.took(exhausted ? 0 : min(n_need, pool_end - pool_next), exhausted);
             if (!exhausted) {
                 const int take = min(n_need, pool_end - pool_next);
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -3099,6 +3141,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
         }
     }
+    wprobe.finish(lane, kBlockChunk / kWave);
     PixStats st;
     lb.to(st);
     publish_stats(out, st, st_err, lane);
@@ -3239,6 +3282,8 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     int an_cnt = kPoolK, ac_cnt = 0;
     int pool_next, pool_end;  // wave-uniform item hand-out
     bool exhausted;
+    WaveProbe wprobe;
+    wprobe.start();
     first_pool(sb, pool_next, pool_end, exhausted);
 
     // the sample's radiance and bounce count to its record; the slot's next phase
@@ -3344,6 +3389,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
             const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
             if (need != 0ull && !exhausted) {
                 if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
+                wprobe.took(exhausted ? 0 : min(__popcll(need), pool_end - pool_next), exhausted);
                 if (!exhausted) {
                     const int take = min(__popcll(need), pool_end - pool_next);
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -3456,6 +3502,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
             }
         }
     }
+    wprobe.finish(lane, kBlockPool / kWave);
     PixStats st;
     lb.to(st);
     publish_stats(out, st, st_err, lane);

@@ -3,6 +3,7 @@
 // the reference's JS doubles do.
 #include "launch.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace rt {
@@ -11,6 +12,19 @@ hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const Rt
                              const LaunchGeom& g, const SampleBuf* sb, hipStream_t stream) {
     return dispatch_render<double>(v, S, reg, out, g, sb, stream);
 }
+
+#if RT_WAVE_PROBE
+// Diagnostic export of the wave probe (RT_WAVE_PROBE=1 variant builds only; pt_kernel.hpp
+// WaveProbe): reset = 1 zeroes it, else copies n words (4 per wave) to host memory.
+extern "C" int rt_debug_wave_probe(unsigned long long* host, int n, int reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_wave_probe)) != hipSuccess) return -1;
+    const size_t words = std::min<size_t>((size_t)std::max(n, 0), (size_t)kWaveProbeSlots * 4);
+    hipError_t e = reset ? hipMemset(p, 0, sizeof(g_wave_probe)) : hipMemcpy(host, p, words * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return e == hipSuccess ? 0 : -1;
+}
+#endif
 
 __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long* counters,
                                   unsigned int* tile_counter) {

@@ -86,7 +86,7 @@ def resources(lib: Path, pattern: str = "") -> list[dict]:
 
 def main():
     root = Path(__file__).resolve().parents[1]
-    lib = Path(sys.argv[1]) if len(sys.argv) > 1 else root / "mcp-raytracer_amd/raytracer_amd/lib/librt_amd.so"
+    lib = Path(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1] else root / "mcp-raytracer_amd/raytracer_amd/lib/librt_amd.so"
     pattern = sys.argv[2] if len(sys.argv) > 2 else ""
     for r in resources(lib, pattern):
         print(f"{r['name'][:90]:90s} vgpr {r['vgpr']:>4} sgpr {r['sgpr']:>4} scratch {r['scratch']:>5} "
