@@ -2694,8 +2694,9 @@ struct AdaptPix {
 struct AdaptRound {
     AdaptPix* state;        // launch slots (tile * 64 + lane)
     int32_t* next_act;      // the pixels still sampling after this round
-    unsigned int* next_count;
+    unsigned int* next_count;  // [0]: pixels carried; [1]: those likely to converge by `horizon`
     int32_t len;            // samples of this round
+    int32_t horizon;        // sample count the round-length rule asks about (rt_api.cpp)
 };
 
 #ifndef RT_REC_NT

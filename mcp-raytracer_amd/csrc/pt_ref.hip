@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
         int i = 0, j = 0;
         const bool valid = a < sb.slots && slot_pixel(sb, reg, tiles_x, rtx, endX, endY, a, i, j);
         const int ls = valid ? (sb.act ? sb.act[a] : sb.tile0 * kWave + a) : 0;
-        bool carry = false;
+        bool carry = false, likely = false;
         if (valid) {
             V3 color = v3(0, 0, 0);
             int n = 0, bmin = 0x7fffffff, bmax = 0;
@@ -200,7 +200,18 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
                 q.b = make_int4((int)(uint32_t)bsum, bmin, bmax, (int)(uint32_t)(bsum >> 32));
                 ar.state[ls] = q;
                 carry = true;
+                // round-length rule only (never a result): would pixelConverged's interval,
+                // 1.96 sqrt(var / n) <= aTolerance * mean at the current mean and variance,
+                // close by n = horizon? (zero or NaN variance: at the next check)
+                const double mean = sIll / n;
+                const double var = n > 1 ? (sIll2 - (sIll * sIll) / n) / (n - 1) : 0.0;
+                likely = !(var > 0.0) ||
+                         (mean > 0.0 && 3.8416 * var <= (double)ar.horizon * C.a_tolerance * C.a_tolerance * mean * mean);
             }
+        }
+        {
+            const unsigned long long ml = __ballot(likely);
+            if (lane == 0 && ml) atomicAdd(ar.next_count + 1, (unsigned int)__popcll(ml));
         }
         // append the carried pixels: one atomic per block and iteration
         const unsigned long long m = __ballot(carry);

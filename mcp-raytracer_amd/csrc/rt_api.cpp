@@ -633,6 +633,14 @@ struct rt_camera {
         // converge at the first check or run to spp) 15.17 -> 14.86 ms with 3 rounds; spheres-500 and
         // rain unchanged at 100; 200 cost rain 47 % (profiles/r03/exp2/)
         const int jump = env_int0("RT_AMD_ADAPT_JUMP", 100);
+        // ... or after a round whose carried pixels are mostly not expected to converge within the
+        // next (grown) round: fewer than RT_AMD_ADAPT_LIKELY per mille of them have a confidence
+        // interval that would close by then at their current mean and variance (pt_adapt_kernel).
+        // Cornell's pixels converge at the first checks or never: 474 of 530,755 carried after round
+        // 1 are likely, so it runs in 2 rounds instead of 3 (14.79 -> 14.45 ms); rain's 20 % and
+        // spheres-500's 11 % keep their rounds; the default scene 13.09 -> 12.96 ms path kernel
+        // (profiles/r05/adaptive_likely/). 0 turns the rule off.
+        const int likely_pm = env_int0("RT_AMD_ADAPT_LIKELY", 100);
         const bool trace = env_flag("RT_AMD_ADAPT_LOG", false);
         adapt_rounds = 0;
         adapt_rendered = 0;
@@ -651,6 +659,7 @@ struct rt_camera {
             if (trace) std::fprintf(stderr, "[rt adaptive] round %d: samples [%d, %d) of %ld pixels\n", adapt_rounds,
                                     s_base, s_base + len, n_act);
             ar.len = len;
+            ar.horizon = (int32_t)std::min<long>(C.n_samples, (long)s_base + len + (long)len * grow);
             ar.next_act = d_act[1 - cur];
             sb.s_base = s_base;
             sb.err_in_rec = 1;
@@ -661,7 +670,7 @@ struct rt_camera {
                 kWave * pass_units((n_act + kWave - 1) / kWave, kWave, chunks_per_slot(sb), rec_per_slot * kWave, sbuf_budget());
             ensure_sbuf((size_t)pass_slots * rec_per_slot);
             sb.rec = d_sbuf;
-            hip_check(hipMemsetAsync(d_acount, 0, sizeof(unsigned int), stream), "hipMemsetAsync");
+            hip_check(hipMemsetAsync(d_acount, 0, 2 * sizeof(unsigned int), stream), "hipMemsetAsync");
             for (long a0 = 0; a0 < n_act; a0 += pass_slots, ++pass) {
                 sb.slots = (int32_t)std::min<long>(pass_slots, n_act - a0);
                 sb.stride_s = sb.slots;
@@ -671,14 +680,20 @@ struct rt_camera {
                 hip_check(launch_adapt(S, reg, out, g.tiles_x, sb, ar, stream), "pt_adapt_kernel launch");
                 hip_check(hipEventRecord(pass_event(pass, 2), stream), "hipEventRecord");
             }
-            hip_check(hipMemcpyAsync(h_acount, d_acount, sizeof(unsigned int), hipMemcpyDeviceToHost, stream),
+            hip_check(hipMemcpyAsync(h_acount, d_acount, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, stream),
                       "hipMemcpyAsync");
             hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
             const long n_prev = n_act;
-            n_act = (long)*h_acount;
+            n_act = (long)h_acount[0];
+            const long n_likely = (long)h_acount[1];
+            if (trace)
+                std::fprintf(stderr, "[rt adaptive]   %ld carried, %ld likely to converge by sample %d\n", n_act, n_likely,
+                             ar.horizon);
             act = d_act[1 - cur];
             cur = 1 - cur;
-            take_rest = jump > 0 && n_act > 0 && (double)(n_prev - n_act) < (double)jump * 1e-3 * (double)n_prev;
+            take_rest = jump > 0 && n_act > 0 &&
+                        ((double)(n_prev - n_act) < (double)jump * 1e-3 * (double)n_prev ||
+                         (likely_pm > 0 && (double)n_likely < (double)likely_pm * 1e-3 * (double)n_act));
         }
     }
 
@@ -691,8 +706,8 @@ struct rt_camera {
     unsigned int* h_acount = nullptr;
     size_t adapt_cap = 0;
     void ensure_adapt(size_t slots) {
-        if (!h_acount) hip_check(hipHostMalloc((void**)&h_acount, sizeof(unsigned int), 0), "hipHostMalloc");
-        if (!d_acount) hip_check(hipMalloc(&d_acount, sizeof(unsigned int)), "hipMalloc");
+        if (!h_acount) hip_check(hipHostMalloc((void**)&h_acount, 2 * sizeof(unsigned int), 0), "hipHostMalloc");
+        if (!d_acount) hip_check(hipMalloc(&d_acount, 2 * sizeof(unsigned int)), "hipMalloc");
         if (slots <= adapt_cap) return;
         free_adapt_buffers();
         hip_check(hipMalloc(&d_astate, slots * sizeof(AdaptPix)), "hipMalloc(adaptive state)");

@@ -352,7 +352,9 @@ def test_adaptive_rounds_ignore_misses_past_convergence(rt, oracle, gpu, path, m
     cam, rgb, rad, st = _render_gpu(rt, sd, ro, region=region)
     assert cam.last_kernel() == ("chunked" if path != "pool" else "pool")
     rounds, rendered = cam.adaptive_info()
-    assert rounds == 3  # the third round, [40, 130), rendered samples 60..129 speculatively
+    # the round in which the pixel converges ([40, 130), or [10, 200) when the round-length rule
+    # takes the rest after round 1) rendered sample 71 - a miss - past the convergence at 60
+    assert rounds in (2, 3) and rendered >= 72
     assert_identical(rad[:1, :1], rgb[:1, :1], orc["radiance"][:1, :1], orc["rgb"][:1, :1], f"slit box {path}")
     assert_stats_identical(st, orc["stats"])
     # fixed spp renders sample 71 for real: the reference's error
