@@ -2046,11 +2046,18 @@ __device__ __forceinline__ unsigned long long wave_max(unsigned long long v) {
     return v;
 }
 
-// pixelConverged (src/camera.ts:348-368), in JS doubles.
+// pixelConverged (src/camera.ts:348-368), in JS doubles. pixel_converged_at_batch is its test
+// for an n already known to satisfy n % aBatch == 0 (pt_adapt_kernel counts down to those n
+// for an integral aBatch instead of an fp64 fmod per sample).
+__device__ __forceinline__ bool pixel_converged_at_batch(const RtCamera& c, int n, double sIll, double sIll2);
 __device__ __forceinline__ bool pixel_converged(const RtCamera& c, int n, double sIll, double sIll2) {
     if (c.a_tolerance <= 0.0 || c.samples <= 1.0 || n < 2) return false;
     const double rem = ::fmod((double)n, c.a_batch);
     if (rem != 0.0) return false;  // also NaN
+    return pixel_converged_at_batch(c, n, sIll, sIll2);
+}
+__device__ __forceinline__ bool pixel_converged_at_batch(const RtCamera& c, int n, double sIll, double sIll2) {
+    if (c.a_tolerance <= 0.0 || c.samples <= 1.0 || n < 2) return false;
     const double mean = sIll / n;
     const double var = (sIll2 - (sIll * sIll) / n) / (n - 1);
     if (var <= 0.0 || var != var) return true;

@@ -172,6 +172,12 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
             }
             bool done = false;
             const float4* rec = sb.rec + (size_t)a * sb.stride_slot;
+            // fmod(n, aBatch) == 0 is n % aBatch == 0 for an integral aBatch: count down to those n
+            // (the fp64 fmod per sample was most of this kernel's arithmetic)
+            const double abd = C.a_batch;
+            const bool ib = abd >= 1.0 && abd < 2147483648.0 && abd == ::floor(abd);
+            const int batch = ib ? (int)abd : 1;
+            int until = ib ? batch - n % batch : 0;  // samples to add until n is the next multiple
             for (int k = 0; k < ar.len && !done; ++k) {
                 // PixelStats.add (renderStats.ts:76-88), then the while condition
                 const float4 r = rec[(size_t)k * sb.stride_s];
@@ -187,7 +193,13 @@ __global__ __launch_bounds__(kAccBlock) void pt_adapt_kernel(DevScene S0, RtRegi
                 const double il = illuminance(c);
                 sIll += il;
                 sIll2 += il * il;
-                done = n >= C.n_samples || pixel_converged(C, n, sIll, sIll2);
+                if (ib) {
+                    const bool check = --until == 0;
+                    if (check) until = batch;
+                    done = n >= C.n_samples || (check && pixel_converged_at_batch(C, n, sIll, sIll2));
+                } else {
+                    done = n >= C.n_samples || pixel_converged(C, n, sIll, sIll2);
+                }
             }
             st_err |= err;
             if (done) {
