@@ -187,7 +187,16 @@ def parse_args(argv):
                     help="rank 0 compares the assembled frame with a single-launch render of the whole image")
     ap.add_argument("--stub", action="store_true",
                     help="CPU rehearsal of the launcher and the gather (gloo, no GPU, no render: tests only)")
-    return ap.parse_args(argv)
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives all N GPUs through the C ABI's rt_camera_render_multi (the call the "
+                         "TypeScript host makes through the N-API addon): host frame out, RCCL gather inside")
+    ap.add_argument("--devices", default="",
+                    help="--single-process: comma-separated device ordinals (default 0..N-1; a repeated ordinal "
+                         "rehearses the N-way split on fewer GPUs)")
+    a = ap.parse_args(argv)
+    if a.repeats < 1 or a.steps < 1 or a.warmup < 0 or a.gpus < 1:
+        ap.error("--repeats and --steps must be >= 1, --warmup >= 0, --gpus >= 1")
+    return a
 
 
 def _load_profile(name: str, key: str):
@@ -248,6 +257,11 @@ def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
     env_world = os.environ.get("WORLD_SIZE")
+    if args.single_process:
+        if env_world not in (None, "1"):
+            print("bench.py: --single-process runs without torch.distributed.run", file=sys.stderr)
+            return 2
+        return single_process_main(args)
     if env_world is None and args.gpus > 1:
         return launch_children(args, argv)
     world_env = int(env_world or "1")
@@ -449,6 +463,99 @@ def main(argv=None):
         dist.barrier()
         dist.destroy_process_group()
     return rc
+
+
+def single_process_main(args) -> int:
+    """--single-process: one process renders each frame over N GPUs with ONE C-ABI call,
+    rt_camera_render_multi (tile groups per device on their own streams, RCCL gather of the
+    tile-packed slabs on devices[0], unpack, merged stats, frame copied into the caller's host
+    buffer) - what the TypeScript host's generateImageBuffer does through the N-API addon's
+    renderRegionMulti (src/raytracer.ts:60-90 replaced by one call). A step = one frame,
+    host buffer included, exactly as the per-rank path's step ends with the host copy."""
+    import numpy as np
+    import torch
+
+    from raytracer_amd import _build
+
+    _build.build_native()
+    import raytracer_amd as rt
+
+    n_vis = rt.device_count()
+    devices = [int(d) for d in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    if len(devices) != args.gpus:
+        print(f"bench.py: --devices lists {len(devices)} ordinals for --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if max(devices) >= n_vis:
+        print(f"bench.py: devices {devices} but {n_vis} visible", file=sys.stderr)
+        return 2
+    cfg, extra, _ = SCENES[args.scene]
+    scene_data = rt.generate_scene_data(cfg)
+    adapt = {"aTolerance": 0.05, "aBatch": 10} if args.adaptive else {"aTolerance": 0}
+    ropts = {"width": args.width, "samples": args.spp, "depth": args.depth, **adapt,
+             "seed": args.seed, "precision": args.precision, "traversal": args.traversal, **extra}
+    cam = rt.create_camera_from_scene_data(scene_data, ropts)
+    W, H = cam.image_width, cam.image_height
+    region = (0, 0, W, H)
+    host_frame = torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True).numpy()
+    log(f"single process: {args.scene} {W}x{H} spp={args.spp} depth={args.depth} on devices {devices} "
+        f"build {rt.build_id()}")
+    for i in range(args.warmup):
+        cam.render_region_multi(host_frame, region, devices)
+        log(f"warmup {i + 1}/{args.warmup}")
+    reps = []
+    for r in range(args.repeats):
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            st = cam.render_region_multi(host_frame, region, devices)  # returns with the frame in host memory
+            if args.steps <= 5 or (i + 1) % 10 == 0:
+                log(f"repeat {r + 1}/{args.repeats}: step {i + 1}/{args.steps}")
+        reps.append(time.perf_counter() - t0)
+    elapsed = sorted(reps)[len(reps) // 2]
+    info = cam.multi_info()
+    timed_rgb = host_frame.copy()
+    kernel_ms = max(info["path_ms"])
+    rad = np.zeros((H, W, 3), np.float32)
+    rgb = np.zeros((H, W, 3), np.uint8)
+    res = cam.render_region_multi(rgb, region, devices, radiance=rad)
+    parity = None if args.no_parity else parity_check(scene_data, ropts, args, timed_rgb, rgb, rad, res)
+    samples_per_step = int(res.samples["total"])
+    value = samples_per_step * args.steps / elapsed / 1e6
+    n_dev = len(set(devices))
+    key = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_{args.precision}_n1" + ("_adaptive" if args.adaptive else "")
+    # one device: the dominant kernel against VALU issue as in the per-rank path; several: the
+    # slowest device's path kernel (its share's counters are not collected separately)
+    rl = (roofline(key, rt.build_id(), samples_per_step, kernel_ms, None, W * H) if len(devices) == 1 else
+          {"bound": "valu", "kernel_ms": round(kernel_ms, 4), "frac": None,
+           "note": "slowest device's path kernel; per-device times in `multi`"})
+    line = {
+        "metric": metric_for(args.scene, W, H, args.spp, args.depth, args.adaptive), "value": round(value, 3),
+        "unit": "Msamples/s", "n_gpus": n_dev, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "repeats": {"n": len(reps), "reported": "median", "ms_per_step": [round(x / args.steps * 1e3, 3) for x in reps]},
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64" if args.precision == "ref" else "f32",
+        "data": f"synthetic: reference scene generator output (deterministic), path RNG seed {args.seed:#x}; no datasets",
+        "config": {"workload": f"{args.scene} {W}x{H} spp={args.spp} depth={args.depth}", "scene": args.scene,
+                   "width": W, "height": H, "spp": args.spp, "depth": args.depth, "precision": args.precision,
+                   "adaptive": adapt if args.adaptive else False, "samples_per_frame": samples_per_step,
+                   "parallelism": f"single process, rt_camera_render_multi over devices {devices}: 8x8-tile "
+                                  f"interleave, {info['transport']} gather of tile-packed slabs on device "
+                                  f"{devices[0]}, host frame out"},
+        "build_id": rt.build_id(),
+        "multi": {"transport": info["transport"], "devices": devices,
+                  "path_ms": [round(x, 4) for x in info["path_ms"]],
+                  "accum_ms": [round(x, 4) for x in info["accum_ms"]], "gather_ms": round(info["gather_ms"], 4),
+                  "slab_tiles": info["slab_tiles"]},
+        "host_copy": "each timed step is one rt_camera_render_multi call returning with the u8 frame in host memory",
+        "parity": parity,
+        "roofline": rl,
+        "cpu_baseline": None,
+    }
+    print(json.dumps(line), flush=True)
+    if parity is not None and not parity["ok"]:
+        log("PARITY FAILURE: the timed frame differs from the oracle")
+        return 3
+    return 0
 
 
 def _stats_equal(a, b) -> bool:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RT_AMD_VERSION 2
+#define RT_AMD_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -222,8 +222,11 @@ int rt_camera_pass_count(rt_camera* cam, int32_t* passes);
 enum { RT_KERNEL_NONE = 0, RT_KERNEL_SEQUENTIAL = 1, RT_KERNEL_CHUNKED = 2, RT_KERNEL_POOL = 3 };
 int rt_camera_last_kernel(rt_camera* cam, int32_t* kernel);
 
-/* Frees the camera's device resources (scene copy, frame and record buffers,
- * events); the next render re-creates them on the then-current device. */
+/* Frees the camera's device resources on every device it rendered on (scene copies, frame,
+ * record and slab buffers, streams, events). A camera otherwise keeps one scene copy per device
+ * (the calling thread's current device for the single-device entries, each listed device for
+ * rt_camera_render_multi), so moving between devices never re-uploads; the next render
+ * re-creates what it needs. */
 int rt_camera_release_device(rt_camera* cam);
 
 /* Hash of the HIP/C++ sources and compiler flags this library was built from
@@ -268,6 +271,66 @@ int rt_debug_png_host(const uint8_t* rgb, int32_t width, int32_t height, uint8_t
  * merged stats (RenderStats.merge) depend on it, so the frame is one launch.
  * *out is malloc'ed (rt_free). */
 int rt_camera_render_png(rt_camera* cam, int32_t bands, rt_render_stats* stats, uint8_t** out, size_t* out_len);
+
+/* ---- Single-process multi-GPU (SURVEY.md §8b "rt_render_multi", §8e) ----------------------
+ * The reference's parallel path is one process driving N workers over bands of one buffer
+ * (src/raytracer.ts:60-90 generateImageBuffer with parallel workers, 185-205
+ * divideIntoRegions; src/render-utils/renderWorker.ts:17-35 each worker's renderRegion,
+ * merged with RenderStats.merge, src/render-utils/renderStats.ts:42-64). Here one call drives
+ * N GPUs: the region's 8x8 tiles are dealt round-robin (tile t -> devices[t % n]); every
+ * listed device renders its tiles into a tile-packed slab on its own stream (one host thread
+ * per device, the camera's scene uploaded once per device and kept); the slabs - each with the
+ * device's RenderStats words in a spare tile - are gathered on devices[0] over RCCL (one
+ * ncclSend / ncclRecv group on single-process communicators, ncclCommInitAll, i.e. xGMI
+ * between MI355X GPUs), unpacked into the full frame by rt_tiles_unpack and the stats merged
+ * as RenderStats.merge does. The path RNG is keyed by (pixel, sample): the image and the
+ * merged stats equal a single-device render bit for bit, for any n. A device may be listed
+ * more than once (the split rehearsed on fewer GPUs); the gather then uses device-to-device
+ * copies (RT_GATHER_PEER), since RCCL needs distinct devices. The environment variable
+ * RT_AMD_GATHER=rccl|peer forces the transport. */
+#define RT_MAX_DEVICES 16
+enum { RT_GATHER_RCCL = 0, RT_GATHER_PEER = 1 };
+
+/* The split of a region over n devices (host only). */
+typedef struct {
+    rt_region region;          /* the region clamped to the image */
+    int32_t n_devices;
+    int32_t slab_tiles;        /* tiles per slab: the largest share, ceil(tiles / n) */
+    int64_t tiles;             /* 8x8 tiles of the region, row-major */
+    int64_t slab_bytes_rgb;    /* u8 slab: (slab_tiles + 1) * 64 * 3 (the spare tile carries the stats words) */
+    int64_t slab_bytes_radiance; /* f32 slab: slab_tiles * 64 * 3 * 4 */
+    int64_t stats_offset;      /* byte offset of the 8 stats words in a u8 slab */
+    int32_t group_tiles[RT_MAX_DEVICES]; /* tiles device entry g renders */
+} rt_multi_plan;
+int rt_multi_plan_region(const rt_region* region, int32_t width, int32_t height, int32_t n_devices,
+                         rt_multi_plan* plan);
+
+/* Camera.renderRegion over n_devices GPUs (see above). rgb / radiance: caller-owned HOST
+ * buffers in full-frame layout as rt_camera_render_region (only the region is written; either
+ * may be NULL); stats: the merged RenderStats (may be NULL). */
+int rt_camera_render_multi(rt_camera* cam, const int32_t* devices, int32_t n_devices, const rt_region* region,
+                           uint8_t* rgb, float* radiance, rt_render_stats* stats);
+
+/* generateImageBuffer over n_devices GPUs: the whole frame as rt_camera_render_multi, then its
+ * PNG encoded on devices[0] (rt_encode_png_device). *out is malloc'ed (rt_free). */
+int rt_camera_render_png_multi(rt_camera* cam, const int32_t* devices, int32_t n_devices, rt_render_stats* stats,
+                               uint8_t** out, size_t* out_len);
+
+/* The most recent rt_camera_render_multi / _png_multi of this camera (n_devices = 0 when a
+ * single-device render came after it): devices, transport, plan, each device's path-kernel and
+ * accumulate time (HIP events on its stream) and gather_ms = devices[0]'s time from the end of
+ * its own render to the assembled frame (waiting for the slowest device, the gather, the unpack
+ * and the stats words' copy). Waits for those events. */
+typedef struct {
+    int32_t n_devices;
+    int32_t transport;         /* RT_GATHER_* */
+    int32_t devices[RT_MAX_DEVICES];
+    float path_ms[RT_MAX_DEVICES];
+    float accum_ms[RT_MAX_DEVICES];
+    float gather_ms;
+    rt_multi_plan plan;
+} rt_multi_info;
+int rt_camera_multi_info(rt_camera* cam, rt_multi_info* info);
 
 #ifdef __cplusplus
 }

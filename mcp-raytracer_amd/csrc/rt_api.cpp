@@ -6,14 +6,22 @@
 // only the region is written, RenderStats are returned.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types and declarations only: librccl is dlopen'ed (Rccl below)
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rt_amd.h"
@@ -129,14 +137,37 @@ static std::vector<RtOnb> planar_onbs(const std::vector<RtPrim>& prims, int32_t*
     return t;
 }
 
-struct rt_camera {
+// The host half of a camera: the reference's Camera after createCameraFromSceneData
+// (src/scenes/scenes.ts:60-104) - the flattened scene, options and mixture weights.
+struct CamHost {
     SceneBuild build;
     int32_t precision = PREC_REF;
     int32_t traversal = TRAV_AUTO;
     double mix_total = 0.5, light_w = 0.0;
-    std::mutex mu;
 
-    int device = -1;
+    // The strategy a launch actually uses: BRUTE/FAST are exact only where every
+    // primitive lies inside its reference box (scene.cpp prims_inside_boxes).
+    int effective_traversal(int trav) const {
+        if (!build.fast_ok) return TRAV_REFERENCE;
+        if (trav == TRAV_AUTO) return build.cam.n_prims <= kBruteMaxPrims ? TRAV_BRUTE : TRAV_FAST;
+        return trav;
+    }
+};
+
+// One device's copy of a camera: the scene blob in that device's HBM, its frame, record and
+// stats buffers, events and (multi-GPU) its stream and tile-packed slabs. A camera keeps one
+// per device it rendered on (rt_camera_render_multi: one per listed device entry), so moving
+// between devices never re-uploads.
+struct DevCtx {
+    const CamHost& host;
+    const SceneBuild& build;
+    const int device;    // HIP device ordinal the buffers live on
+    const int instance;  // >0: a further context on the same device (a device listed twice)
+    bool live = false;   // scene uploaded, buffers allocated
+    DevCtx(const CamHost& h, int dev, int inst) : host(h), build(h.build), device(dev), instance(inst) {}
+    DevCtx(const DevCtx&) = delete;
+    DevCtx& operator=(const DevCtx&) = delete;
+
     uint4* d_blob = nullptr;  // [tnodes][prims][mats][lights][nodes] (DevScene)
     int32_t lds_words = 0;    // [tnodes][tprims][tsph][prims] prefix, 16-byte words
     int32_t lds_words2 = 0;   // the same + [mats][lights]
@@ -159,10 +190,64 @@ struct rt_camera {
     float* d_rad = nullptr;
     int cus = 256;
 
-    ~rt_camera() { release(); }
+    // multi-GPU (rt_camera_render_multi): this context's stream, its tile-packed slabs, and on
+    // the root context the gathered slabs of every device plus the stats words' host copy
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_rendered = nullptr, ev_gather0 = nullptr, ev_gather1 = nullptr;
+    uint8_t* d_slab = nullptr;
+    float* d_rslab = nullptr;
+    uint8_t* d_gather = nullptr;
+    float* d_rgather = nullptr;
+    size_t slab_cap = 0, rslab_cap = 0, gather_cap = 0, rgather_cap = 0;
+    unsigned long long* h_words = nullptr;
+    int h_words_cap = 0;
+
+    ~DevCtx() {
+        release();
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(device);
+        for (void* p : {(void*)d_slab, (void*)d_rslab, (void*)d_gather, (void*)d_rgather})
+            if (p) (void)hipFree(p);
+        if (h_words) (void)hipHostFree(h_words);
+        for (hipEvent_t e : {ev_rendered, ev_gather0, ev_gather1})
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+        (void)hipSetDevice(prev);
+    }
+
+    // multi-GPU buffers (grown on demand; the caller has made `device` current)
+    template <class T>
+    static T* grow(T* p, size_t& cap, size_t bytes, const char* what) {
+        if (bytes <= cap && p) return p;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hip_check(hipMalloc(&p, std::max<size_t>(bytes, 16)), what);
+        cap = bytes;
+        return p;
+    }
+    void ensure_multi(size_t slab_bytes, size_t rslab_bytes, bool root, int n) {
+        if (!stream) hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+        for (hipEvent_t* e : {&ev_rendered, &ev_gather0, &ev_gather1})
+            if (!*e) hip_check(hipEventCreate(e), "hipEventCreate");
+        d_slab = grow(d_slab, slab_cap, slab_bytes, "hipMalloc(slab)");
+        if (rslab_bytes) d_rslab = grow(d_rslab, rslab_cap, rslab_bytes, "hipMalloc(radiance slab)");
+        if (!root) return;
+        d_gather = grow(d_gather, gather_cap, slab_bytes * n, "hipMalloc(gathered slabs)");
+        if (rslab_bytes) d_rgather = grow(d_rgather, rgather_cap, rslab_bytes * n, "hipMalloc(gathered radiance)");
+        if (h_words_cap < n) {
+            if (h_words) (void)hipHostFree(h_words);
+            h_words = nullptr;
+            h_words_cap = 0;
+            hip_check(hipHostMalloc((void**)&h_words, (size_t)n * ST_WORDS * sizeof(unsigned long long), 0),
+                      "hipHostMalloc");
+            h_words_cap = n;
+        }
+    }
 
     void release() {
-        if (device < 0) return;
+        if (!live) return;
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -189,7 +274,7 @@ struct rt_camera {
         ev.clear();
         n_passes = 0;
         (void)hipSetDevice(prev);
-        device = -1;
+        live = false;
     }
 
     // RtPre (scene.hpp) of every primitive, from its RtPrim fields
@@ -234,11 +319,12 @@ struct rt_camera {
         blob.insert(blob.end(), p, p + v.size() * sizeof(T));
     }
 
+    // Uploads the scene on first use; the caller has made `device` current.
     void ensure_device() {
         int dev = 0;
         hip_check(hipGetDevice(&dev), "hipGetDevice");
-        if (device == dev) return;
-        if (device >= 0) release();
+        if (dev != device) throw std::logic_error("device context used on another device");
+        if (live) return;
         std::vector<char> blob;
         if (RT_BVH4) append(blob, build.t4nodes, nullptr);  // the fast traversal's tree heads the blob
         else append(blob, build.tnodes, nullptr);
@@ -262,7 +348,7 @@ struct rt_camera {
         hip_check(hipMalloc(&d_stats, ST_WORDS * kStatStride * sizeof(unsigned long long)), "hipMalloc");
         hip_check(hipMalloc(&d_counters, kCounterWords * sizeof(unsigned long long)), "hipMalloc");
         hip_check(hipMalloc(&d_tile, 64), "hipMalloc");
-        device = dev;
+        live = true;
         cus = device_cus(dev);
         int smem = 0;
         if (hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && smem > 0)
@@ -288,10 +374,24 @@ struct rt_camera {
 
     // The strategy a launch actually uses: BRUTE/FAST are exact only where every
     // primitive lies inside its reference box (scene.cpp prims_inside_boxes).
-    int effective_traversal(int trav) const {
-        if (!build.fast_ok) return TRAV_REFERENCE;
-        if (trav == TRAV_AUTO) return build.cam.n_prims <= kBruteMaxPrims ? TRAV_BRUTE : TRAV_FAST;
-        return trav;
+    int effective_traversal(int trav) const { return host.effective_traversal(trav); }
+
+    // Device time of the last launch from its events: path kernel(s) and accumulate passes,
+    // summed per pass (never one span across both). Waits for those events.
+    void times(float* path_ms, float* accum_ms) {
+        *path_ms = 0.0f;
+        *accum_ms = 0.0f;
+        for (int p = 0; p < n_passes; ++p) {
+            float a = 0.0f, b = 0.0f;
+            hip_check(hipEventSynchronize(ev[3 * p + 1]), "hipEventSynchronize");
+            hip_check(hipEventElapsedTime(&a, ev[3 * p], ev[3 * p + 1]), "hipEventElapsedTime");
+            *path_ms += a;
+            if (ev_accum) {
+                hip_check(hipEventSynchronize(ev[3 * p + 2]), "hipEventSynchronize");
+                hip_check(hipEventElapsedTime(&b, ev[3 * p + 1], ev[3 * p + 2]), "hipEventElapsedTime");
+                *accum_ms += b;
+            }
+        }
     }
 
     DevScene dev_scene() const {
@@ -330,8 +430,8 @@ struct rt_camera {
         S.troot = RT_BVH4 ? build.t4root : build.troot;
         S.root_box = build.troot_box;
         S.cam = build.cam;
-        S.mix_total = mix_total;
-        S.light_w = light_w;
+        S.mix_total = host.mix_total;
+        S.light_w = host.light_w;
         return S;
     }
 
@@ -755,6 +855,11 @@ struct rt_camera {
         for (int k = 0; k < ST_WORDS; ++k) w[k] = wl[k * kStatStride];
         if (counters)
             for (int k = 0; k < kCounterWords; ++k) counters[k] = c[k];
+        stats_from_words(w, st);
+    }
+
+    // RenderStats from the 8 stats words; the reference's thrown Errors for the error flags.
+    static void stats_from_words(const unsigned long long* w, rt_render_stats* st) {
         if (w[ST_ERROR] & ERR_NO_BACKGROUND)
             throw std::runtime_error("Cannot read properties of undefined (reading 'top')");
         if (w[ST_ERROR] & ERR_EMIT_STACK)
@@ -771,6 +876,308 @@ struct rt_camera {
         st->bounces_avg = st->samples_total > 0 ? st->bounces_total / st->samples_total : 0.0;
     }
 };
+
+// RenderStats.merge (src/render-utils/renderStats.ts:42-64) over the stats words of n
+// renders (row r at words + r * ST_WORDS): totals summed, minima / maxima over the renders
+// (~0 = no sample: skipped by the unsigned minimum), error flags or'ed.
+static void merge_stats_words(const unsigned long long* words, int n, unsigned long long* m) {
+    m[ST_PIXELS] = m[ST_SAMPLES] = m[ST_BOUNCES] = m[ST_SMAX] = m[ST_BMAX] = m[ST_ERROR] = 0;
+    m[ST_SMIN] = m[ST_BMIN] = ~0ull;
+    for (int r = 0; r < n; ++r) {
+        const unsigned long long* w = words + (size_t)r * ST_WORDS;
+        m[ST_PIXELS] += w[ST_PIXELS];
+        m[ST_SAMPLES] += w[ST_SAMPLES];
+        m[ST_BOUNCES] += w[ST_BOUNCES];
+        m[ST_SMIN] = std::min(m[ST_SMIN], w[ST_SMIN]);
+        m[ST_BMIN] = std::min(m[ST_BMIN], w[ST_BMIN]);
+        m[ST_SMAX] = std::max(m[ST_SMAX], w[ST_SMAX]);
+        m[ST_BMAX] = std::max(m[ST_BMAX], w[ST_BMAX]);
+        m[ST_ERROR] |= w[ST_ERROR];
+    }
+}
+
+// The multi-GPU split of a region: its 8x8 tiles dealt round-robin over n
+// devices (tile t -> entry t % n), each device's tiles packed into an equal-size slab padded
+// to the largest share, plus one spare tile whose first 64 bytes carry the device's stats
+// words (the gather brings them along; rt_tiles_unpack never reads that tile).
+static rt_multi_plan make_multi_plan(const rt_region& region, int width, int height, int n) {
+    rt_multi_plan p{};
+    const int x0 = std::max(region.x, 0), y0 = std::max(region.y, 0);
+    const int x1 = std::min(region.x + region.width, width), y1 = std::min(region.y + region.height, height);
+    p.region = rt_region{x0, y0, std::max(x1 - x0, 0), std::max(y1 - y0, 0)};
+    p.n_devices = n;
+    p.tiles = (int64_t)((p.region.width + kTile - 1) / kTile) * ((p.region.height + kTile - 1) / kTile);
+    p.slab_tiles = (int32_t)((p.tiles + n - 1) / n);
+    p.slab_bytes_rgb = (int64_t)(p.slab_tiles + 1) * kWave * 3;
+    p.slab_bytes_radiance = (int64_t)p.slab_tiles * kWave * 3 * (int64_t)sizeof(float);
+    p.stats_offset = (int64_t)p.slab_tiles * kWave * 3;
+    for (int g = 0; g < n && g < RT_MAX_DEVICES; ++g)
+        p.group_tiles[g] = (int32_t)(p.tiles > g ? (p.tiles - g + n - 1) / n : 0);
+    return p;
+}
+
+// RCCL, loaded at the first multi-GPU gather (dlopen: a process that already holds PyTorch's
+// librccl.so.1 shares it; a Node host loads ROCm's). Single-process communicators over the
+// listed devices (ncclCommInitAll), cached per device list for the life of the process.
+struct Rccl {
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::mutex mu;  // one gather at a time per process (a communicator is not re-entrant)
+    std::vector<std::pair<std::vector<int>, std::vector<ncclComm_t>>> comms;
+
+    void check(ncclResult_t r, const char* what) {
+        if (r != ncclSuccess) throw HipError(std::string(what) + ": " + (error_string ? error_string(r) : "RCCL error"));
+    }
+    const std::vector<ncclComm_t>& comms_for(const std::vector<int>& devs) {
+        for (auto& c : comms)
+            if (c.first == devs) return c.second;
+        std::vector<ncclComm_t> cs(devs.size(), nullptr);
+        check(comm_init_all(cs.data(), (int)devs.size(), devs.data()), "ncclCommInitAll");
+        comms.emplace_back(devs, std::move(cs));
+        return comms.back().second;
+    }
+};
+
+static Rccl& rccl() {
+    static std::mutex load_mu;
+    static Rccl* lib = nullptr;
+    static std::string load_error;
+    std::lock_guard<std::mutex> lock(load_mu);
+    if (lib) return *lib;
+    if (!load_error.empty()) throw HipError(load_error);
+    const char* env = std::getenv("RT_AMD_RCCL_LIB");
+    void* h = nullptr;
+    for (const char* name : {env && env[0] ? env : "librccl.so.1", "librccl.so"})
+        if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!h) {
+        load_error = std::string("RCCL not loadable (librccl.so.1): ") + dlerror() +
+                     " - set RT_AMD_GATHER=peer for device-to-device copies";
+        throw HipError(load_error);
+    }
+    auto* r = new Rccl();
+    auto sym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        if (!fn) load_error = std::string("RCCL symbol missing: ") + name;
+    };
+    sym(r->comm_init_all, "ncclCommInitAll");
+    sym(r->group_start, "ncclGroupStart");
+    sym(r->group_end, "ncclGroupEnd");
+    sym(r->send, "ncclSend");
+    sym(r->recv, "ncclRecv");
+    sym(r->error_string, "ncclGetErrorString");
+    if (!load_error.empty()) {
+        delete r;
+        throw HipError(load_error);
+    }
+    lib = r;
+    return *lib;
+}
+
+struct rt_camera : CamHost {
+    std::mutex mu;
+    std::vector<std::unique_ptr<DevCtx>> ctxs;
+    DevCtx* last = nullptr;  // the context of the most recent render (queries read it)
+    // the most recent rt_camera_render_multi: its device contexts, transport and plan
+    std::vector<DevCtx*> multi;
+    int multi_transport = -1;
+    rt_multi_plan multi_plan{};
+
+    DevCtx& ctx(int dev, int inst = 0) {
+        for (auto& c : ctxs)
+            if (c->device == dev && c->instance == inst) return *c;
+        ctxs.emplace_back(new DevCtx(*this, dev, inst));
+        return *ctxs.back();
+    }
+    // the context of the calling thread's current HIP device
+    DevCtx& current() {
+        int dev = 0;
+        hip_check(hipGetDevice(&dev), "hipGetDevice");
+        return ctx(dev, 0);
+    }
+    void release() {
+        multi.clear();
+        last = nullptr;
+        ctxs.clear();
+    }
+};
+
+// The current HIP device of the calling thread, restored when the scope ends.
+struct DeviceScope {
+    int prev = 0;
+    DeviceScope() { (void)hipGetDevice(&prev); }
+    ~DeviceScope() { (void)hipSetDevice(prev); }
+};
+
+// Single-process multi-GPU render (rt_camera_render_multi). Entry g of `devs` renders tile
+// group g of n into its context's tile-packed slab on its own stream (one host thread per entry,
+// so renders that wait on the host between rounds - adaptive sampling - still overlap); the
+// slabs are gathered on devs[0] (RCCL send / recv in one group over xGMI, or device-to-device
+// copies), unpacked into devs[0]'s full frame (rt_tiles_unpack) and the stats words merged as
+// RenderStats.merge does (the reference's workers: src/raytracer.ts:60-90, 185-205;
+// src/render-utils/renderWorker.ts:17-35). Returns the root context with the frame in
+// d_rgb / d_rad: `outputs` queues the caller's copies on its stream before the one host
+// sync, after which *merged holds the merged stats words.
+static DevCtx& render_multi(rt_camera* cam, const int32_t* devices, int n, const rt_region& region, bool want_rgb,
+                            bool want_rad, unsigned long long* merged, const std::function<void(DevCtx&)>& outputs) {
+    int count = 0;
+    hip_check(hipGetDeviceCount(&count), "hipGetDeviceCount");
+    if (n < 1 || n > RT_MAX_DEVICES || !devices)
+        throw std::invalid_argument("rt_camera_render_multi: 1 <= n_devices <= RT_MAX_DEVICES devices are required");
+    std::vector<int> devs(devices, devices + n);
+    bool distinct = true;
+    for (int g = 0; g < n; ++g) {
+        if (devs[g] < 0 || devs[g] >= count)
+            throw std::invalid_argument("rt_camera_render_multi: device " + std::to_string(devs[g]) + " is not visible (" +
+                                        std::to_string(count) + " devices)");
+        for (int h = 0; h < g; ++h) distinct = distinct && devs[h] != devs[g];
+    }
+    // transport: RCCL over xGMI when every entry is its own device, else device-to-device
+    // copies (a device listed twice: the split rehearsed on fewer GPUs; RCCL refuses that)
+    const char* ge = std::getenv("RT_AMD_GATHER");
+    const std::string gs = ge ? ge : "";
+    int transport = distinct ? RT_GATHER_RCCL : RT_GATHER_PEER;
+    if (gs == "peer") transport = RT_GATHER_PEER;
+    else if (gs == "rccl") transport = RT_GATHER_RCCL;
+    else if (!gs.empty()) throw std::invalid_argument("RT_AMD_GATHER must be 'rccl' or 'peer'");
+    if (transport == RT_GATHER_RCCL && !distinct)
+        throw std::invalid_argument("rt_camera_render_multi: RCCL needs distinct devices (RT_AMD_GATHER=peer allows repeats)");
+
+    const RtCamera& C = cam->build.cam;
+    const rt_multi_plan plan = make_multi_plan(region, C.width, C.height, n);
+    std::vector<DevCtx*> cs(n);
+    for (int g = 0; g < n; ++g) {
+        int inst = 0;
+        for (int h = 0; h < g; ++h) inst += devs[h] == devs[g];
+        cs[g] = &cam->ctx(devs[g], inst);
+    }
+    cam->multi = cs;
+    cam->multi_transport = transport;
+    cam->multi_plan = plan;
+    const size_t slab_b = (size_t)plan.slab_bytes_rgb, rslab_b = want_rad ? (size_t)plan.slab_bytes_radiance : 0;
+    DeviceScope scope;
+
+    // renders: one host thread per further entry, entry 0 on the calling thread
+    std::vector<std::exception_ptr> errs(n);
+    auto work = [&](int g) {
+        try {
+            DevCtx& c = *cs[g];
+            hip_check(hipSetDevice(c.device), "hipSetDevice");
+            c.ensure_device();
+            c.ensure_multi(slab_b, rslab_b, g == 0, n);
+            if (g == 0) c.ensure_frame();
+            c.launch(plan.region, g, n, cam->precision, cam->traversal, 0, c.d_slab, want_rad ? c.d_rslab : nullptr,
+                     nullptr, nullptr, 1, c.stream);
+            // the stats words into the slab's spare tile (rides in the gather)
+            hip_check(hipMemcpy2DAsync(c.d_slab + plan.stats_offset, sizeof(unsigned long long), c.d_stats,
+                                       kStatStride * sizeof(unsigned long long), sizeof(unsigned long long), ST_WORDS,
+                                       hipMemcpyDeviceToDevice, c.stream),
+                      "hipMemcpy2DAsync(stats)");
+            hip_check(hipEventRecord(c.ev_rendered, c.stream), "hipEventRecord");
+        } catch (...) {
+            errs[g] = std::current_exception();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int g = 1; g < n; ++g) th.emplace_back(work, g);
+    work(0);
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+
+    DevCtx& root = *cs[0];
+    hip_check(hipSetDevice(root.device), "hipSetDevice");
+    hip_check(hipEventRecord(root.ev_gather0, root.stream), "hipEventRecord");
+    if (transport == RT_GATHER_RCCL) {
+        Rccl& r = rccl();
+        std::lock_guard<std::mutex> lock(r.mu);
+        const std::vector<ncclComm_t>& comms = r.comms_for(devs);
+        // one group: entry g sends its slab(s) to rank 0, rank 0 receives slab g into row g
+        // (rank 0's own slab included: a send / recv pair to itself)
+        r.check(r.group_start(), "ncclGroupStart");
+        for (int g = 0; g < n; ++g) {
+            r.check(r.send(cs[g]->d_slab, slab_b, ncclUint8, 0, comms[g], cs[g]->stream), "ncclSend");
+            if (want_rad) r.check(r.send(cs[g]->d_rslab, rslab_b / sizeof(float), ncclFloat32, 0, comms[g], cs[g]->stream),
+                                  "ncclSend");
+        }
+        for (int g = 0; g < n; ++g) {
+            r.check(r.recv(root.d_gather + (size_t)g * slab_b, slab_b, ncclUint8, g, comms[0], root.stream), "ncclRecv");
+            if (want_rad)
+                r.check(r.recv(root.d_rgather + (size_t)g * (rslab_b / sizeof(float)), rslab_b / sizeof(float),
+                               ncclFloat32, g, comms[0], root.stream),
+                        "ncclRecv");
+        }
+        r.check(r.group_end(), "ncclGroupEnd");
+    } else {
+        for (int g = 0; g < n; ++g) {
+            hip_check(hipStreamWaitEvent(root.stream, cs[g]->ev_rendered, 0), "hipStreamWaitEvent");
+            hip_check(hipMemcpyPeerAsync(root.d_gather + (size_t)g * slab_b, root.device, cs[g]->d_slab, cs[g]->device,
+                                         slab_b, root.stream),
+                      "hipMemcpyPeerAsync");
+            if (want_rad)
+                hip_check(hipMemcpyPeerAsync(root.d_rgather + (size_t)g * (rslab_b / sizeof(float)), root.device,
+                                             cs[g]->d_rslab, cs[g]->device, rslab_b, root.stream),
+                          "hipMemcpyPeerAsync");
+        }
+        // an entry's next render must not overwrite its slab before this copy has read it
+        hip_check(hipEventRecord(root.ev_rendered, root.stream), "hipEventRecord");
+        for (int g = 1; g < n; ++g) {
+            hip_check(hipSetDevice(cs[g]->device), "hipSetDevice");
+            hip_check(hipStreamWaitEvent(cs[g]->stream, root.ev_rendered, 0), "hipStreamWaitEvent");
+        }
+        hip_check(hipSetDevice(root.device), "hipSetDevice");
+    }
+    const RtRegion reg{plan.region.x, plan.region.y, plan.region.width, plan.region.height, 0, 1};
+    if (want_rgb)
+        hip_check(launch_tiles_unpack(root.d_gather, n, plan.slab_tiles + 1, reg, C.width, 3, 1, root.d_rgb, root.stream),
+                  "tiles_unpack_kernel");
+    if (want_rad)
+        hip_check(launch_tiles_unpack(root.d_rgather, n, plan.slab_tiles, reg, C.width, 3, 4, root.d_rad, root.stream),
+                  "tiles_unpack_kernel");
+    hip_check(hipMemcpy2DAsync(root.h_words, ST_WORDS * sizeof(unsigned long long), root.d_gather + plan.stats_offset, slab_b,
+                               ST_WORDS * sizeof(unsigned long long), n, hipMemcpyDeviceToHost, root.stream),
+              "hipMemcpy2DAsync(stats words)");
+    hip_check(hipEventRecord(root.ev_gather1, root.stream), "hipEventRecord");
+    if (outputs) outputs(root);  // the caller's copies / encode, queued before the one sync
+    hip_check(hipStreamSynchronize(root.stream), "hipStreamSynchronize");
+    merge_stats_words(root.h_words, n, merged);
+    cam->last = &root;
+    return root;
+}
+
+// Queues the copy of a region's rows of the context's full frame into the caller's host
+// buffers (full-frame layout: only the region is written, as Camera.renderRegion does).
+static void copy_region_to_host(DevCtx& c, const rt_region& region, uint8_t* rgb, float* radiance, hipStream_t stream) {
+    const RtCamera& C = c.build.cam;
+    const int x0 = std::max(region.x, 0), y0 = std::max(region.y, 0);
+    const int x1 = std::min(region.x + region.width, C.width);
+    const int y1 = std::min(region.y + region.height, C.height);
+    if (x1 <= x0 || y1 <= y0) return;
+    const size_t pitch = (size_t)C.width * 3;
+    const size_t off = ((size_t)y0 * C.width + x0) * 3;
+    const size_t w = (size_t)(x1 - x0) * 3;
+    if (rgb)
+        hip_check(hipMemcpy2DAsync(rgb + off, pitch, c.d_rgb + off, pitch, w, y1 - y0, hipMemcpyDeviceToHost, stream),
+                  "hipMemcpy2DAsync");
+    if (radiance)
+        hip_check(hipMemcpy2DAsync(radiance + off, pitch * sizeof(float), c.d_rad + off, pitch * sizeof(float),
+                                   w * sizeof(float), y1 - y0, hipMemcpyDeviceToHost, stream),
+                  "hipMemcpy2DAsync");
+}
+
+// The frame's PNG: encoded on the device from the context's u8 frame (png.hip), malloc'ed.
+static void png_out(DevCtx& c, hipStream_t stream, uint8_t** out, size_t* out_len) {
+    const RtCamera& C = c.build.cam;
+    const std::vector<uint8_t> png = rt_png_encode_device(c.d_rgb, C.width, C.height, stream);
+    uint8_t* b = (uint8_t*)std::malloc(png.size());
+    if (!b) throw std::runtime_error("out of memory");
+    std::memcpy(b, png.data(), png.size());
+    *out = b;
+    *out_len = png.size();
+}
 
 extern "C" {
 
@@ -907,29 +1314,17 @@ int rt_camera_render_region(rt_camera* cam, const rt_region* region, uint8_t* rg
     if (!cam || !region) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
     try {
-        cam->ensure_device();
-        cam->ensure_frame();
-        const RtCamera& C = cam->build.cam;
+        DevCtx& c = cam->current();
+        c.ensure_device();
+        c.ensure_frame();
         const hipStream_t stream = nullptr;
-        cam->launch(*region, 0, 1, cam->precision, cam->traversal, 0, rgb ? cam->d_rgb : nullptr,
-                    radiance ? cam->d_rad : nullptr, nullptr, nullptr, 0, stream);
-        cam->read_stats(stats, nullptr, stream);
-        // copy back only the region's rows/columns (the caller's buffer is the full frame)
-        const int x0 = std::max(region->x, 0), y0 = std::max(region->y, 0);
-        const int x1 = std::min(region->x + region->width, C.width);
-        const int y1 = std::min(region->y + region->height, C.height);
-        if (x1 > x0 && y1 > y0) {
-            const size_t pitch = (size_t)C.width * 3;
-            const size_t off = ((size_t)y0 * C.width + x0) * 3;
-            const size_t w = (size_t)(x1 - x0) * 3;
-            if (rgb)
-                hip_check(hipMemcpy2D(rgb + off, pitch, cam->d_rgb + off, pitch, w, y1 - y0, hipMemcpyDeviceToHost),
-                          "hipMemcpy2D");
-            if (radiance)
-                hip_check(hipMemcpy2D(radiance + off, pitch * sizeof(float), cam->d_rad + off, pitch * sizeof(float),
-                                      w * sizeof(float), y1 - y0, hipMemcpyDeviceToHost),
-                          "hipMemcpy2D");
-        }
+        cam->last = &c;
+        cam->multi.clear();
+        c.launch(*region, 0, 1, cam->precision, cam->traversal, 0, rgb ? c.d_rgb : nullptr,
+                 radiance ? c.d_rad : nullptr, nullptr, nullptr, 0, stream);
+        c.read_stats(stats, nullptr, stream);
+        copy_region_to_host(c, *region, rgb, radiance, stream);
+        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
         return RT_OK;
     } catch (const HipError& e) {
         return set_error(RT_ERR_DEVICE, e.what());
@@ -950,8 +1345,9 @@ int rt_camera_render_png(rt_camera* cam, int32_t bands, rt_render_stats* stats, 
     if (!cam || !out || !out_len) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
     try {
-        cam->ensure_device();
-        cam->ensure_frame();
+        DevCtx& c = cam->current();
+        c.ensure_device();
+        c.ensure_frame();
         const RtCamera& C = cam->build.cam;
         const hipStream_t stream = nullptr;
         // The reference renders divideIntoRegions' ceil(H / count)-row bands on `count` workers
@@ -962,16 +1358,13 @@ int rt_camera_render_png(rt_camera* cam, int32_t bands, rt_render_stats* stats, 
         // instead of `bands` small ones, each waiting for the GPU.
         (void)bands;
         const rt_region r{0, 0, C.width, C.height};
-        cam->launch(r, 0, 1, cam->precision, cam->traversal, 0, cam->d_rgb, nullptr, nullptr, nullptr, 0, stream);
+        cam->last = &c;
+        cam->multi.clear();
+        c.launch(r, 0, 1, cam->precision, cam->traversal, 0, c.d_rgb, nullptr, nullptr, nullptr, 0, stream);
         rt_render_stats m;
-        cam->read_stats(&m, nullptr, stream);
+        c.read_stats(&m, nullptr, stream);
         if (stats) *stats = m;
-        const std::vector<uint8_t> png = rt_png_encode_device(cam->d_rgb, C.width, C.height, stream);
-        uint8_t* b = (uint8_t*)std::malloc(png.size());
-        if (!b) throw std::runtime_error("out of memory");
-        std::memcpy(b, png.data(), png.size());
-        *out = b;
-        *out_len = png.size();
+        png_out(c, stream, out, out_len);
         return RT_OK;
     } catch (const HipError& e) {
         return set_error(RT_ERR_DEVICE, e.what());
@@ -986,14 +1379,17 @@ int rt_camera_render_device(rt_camera* cam, const rt_launch* L, rt_render_stats*
     if (!cam || !L) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
     try {
-        cam->ensure_device();
+        DevCtx& c = cam->current();
+        c.ensure_device();
         const hipStream_t stream = (hipStream_t)L->stream;
         const int prec = L->precision < 0 ? cam->precision : L->precision;
         const int trav = L->traversal < 0 ? cam->traversal : L->traversal;
         if (L->count_work < 0 || L->count_work > 2) throw std::invalid_argument("count_work must be 0, 1 or 2");
-        cam->launch(L->region, L->tile_group, L->tile_groups, prec, trav, L->count_work, L->rgb, L->radiance,
-                    L->px_samples, L->px_bounces, L->packed_tiles, stream);
-        if (L->synchronize) cam->read_stats(stats, L->count_work ? work_counters : nullptr, stream);
+        cam->last = &c;
+        cam->multi.clear();
+        c.launch(L->region, L->tile_group, L->tile_groups, prec, trav, L->count_work, L->rgb, L->radiance,
+                 L->px_samples, L->px_bounces, L->packed_tiles, stream);
+        if (L->synchronize) c.read_stats(stats, L->count_work ? work_counters : nullptr, stream);
         return RT_OK;
     } catch (const HipError& e) {
         return set_error(RT_ERR_DEVICE, e.what());
@@ -1024,15 +1420,16 @@ int rt_debug_world_hit(rt_camera* cam, int32_t traversal, int32_t n, const float
     float* d_d = nullptr;
     double* d_out = nullptr;
     try {
-        cam->ensure_device();
+        DevCtx& c = cam->current();
+        c.ensure_device();
         if (n == 0) return RT_OK;
         hip_check(hipMalloc(&d_o, (size_t)n * 3 * sizeof(float)), "hipMalloc");
         hip_check(hipMalloc(&d_d, (size_t)n * 3 * sizeof(float)), "hipMalloc");
         hip_check(hipMalloc(&d_out, (size_t)n * 10 * sizeof(double)), "hipMalloc");
         hip_check(hipMemcpy(d_o, orig, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
         hip_check(hipMemcpy(d_d, dir, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
-        const int trav = cam->effective_traversal(traversal < 0 ? cam->traversal : traversal);
-        hip_check(launch_world_hit_ref(cam->dev_scene(), trav, n, d_o, d_d, d_out, nullptr),
+        const int trav = c.effective_traversal(traversal < 0 ? cam->traversal : traversal);
+        hip_check(launch_world_hit_ref(c.dev_scene(), trav, n, d_o, d_d, d_out, nullptr),
                   "world_hit_kernel");
         hip_check(hipMemcpy(out, d_out, (size_t)n * 10 * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
         (void)hipFree(d_o);
@@ -1118,18 +1515,7 @@ int rt_camera_kernel_times(rt_camera* cam, float* path_ms, float* accum_ms) {
     try {
         *path_ms = 0.0f;
         *accum_ms = 0.0f;
-        // summed per pass: path kernel time and accumulate time, never one span across both
-        for (int p = 0; p < cam->n_passes; ++p) {
-            float a = 0.0f, b = 0.0f;
-            hip_check(hipEventSynchronize(cam->ev[3 * p + 1]), "hipEventSynchronize");
-            hip_check(hipEventElapsedTime(&a, cam->ev[3 * p], cam->ev[3 * p + 1]), "hipEventElapsedTime");
-            *path_ms += a;
-            if (cam->ev_accum) {
-                hip_check(hipEventSynchronize(cam->ev[3 * p + 2]), "hipEventSynchronize");
-                hip_check(hipEventElapsedTime(&b, cam->ev[3 * p + 1], cam->ev[3 * p + 2]), "hipEventElapsedTime");
-                *accum_ms += b;
-            }
-        }
+        if (cam->last) cam->last->times(path_ms, accum_ms);
         return RT_OK;
     } catch (const std::exception& e) {
         return set_error(RT_ERR_DEVICE, e.what());
@@ -1140,9 +1526,10 @@ int rt_camera_stats_words(rt_camera* cam, uint64_t* dst, void* stream) {
     if (!cam || !dst) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
     try {
-        if (cam->device < 0 || !cam->d_stats) throw std::invalid_argument("rt_camera_stats_words: no render yet");
+        DevCtx* c = cam->last;
+        if (!c || !c->live || !c->d_stats) throw std::invalid_argument("rt_camera_stats_words: no render yet");
         // the ST_WORDS words sit kStatStride apart (one 128-B line each); dst gets them packed
-        hip_check(hipMemcpy2DAsync(dst, sizeof(uint64_t), cam->d_stats, kStatStride * sizeof(unsigned long long),
+        hip_check(hipMemcpy2DAsync(dst, sizeof(uint64_t), c->d_stats, kStatStride * sizeof(unsigned long long),
                                    sizeof(uint64_t), ST_WORDS, hipMemcpyDeviceToDevice, (hipStream_t)stream),
                   "hipMemcpy2DAsync(stats)");
         return RT_OK;
@@ -1156,23 +1543,89 @@ int rt_camera_stats_words(rt_camera* cam, uint64_t* dst, void* stream) {
 int rt_camera_adaptive_info(rt_camera* cam, int32_t* rounds, uint64_t* samples_rendered) {
     if (!cam || !rounds || !samples_rendered) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
-    *rounds = cam->adapt_rounds;
-    *samples_rendered = cam->adapt_rendered;
+    *rounds = cam->last ? cam->last->adapt_rounds : 0;
+    *samples_rendered = cam->last ? cam->last->adapt_rendered : 0;
     return RT_OK;
 }
 
 int rt_camera_pass_count(rt_camera* cam, int32_t* passes) {
     if (!cam || !passes) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
-    *passes = cam->n_passes;
+    *passes = cam->last ? cam->last->n_passes : 0;
     return RT_OK;
 }
 
 int rt_camera_last_kernel(rt_camera* cam, int32_t* kernel) {
     if (!cam || !kernel) return set_error(RT_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lock(cam->mu);
-    *kernel = cam->last_kernel;
+    *kernel = cam->last ? cam->last->last_kernel : RT_KERNEL_NONE;
     return RT_OK;
+}
+
+int rt_multi_plan_region(const rt_region* region, int32_t width, int32_t height, int32_t n_devices,
+                         rt_multi_plan* plan) {
+    if (!region || !plan || width < 0 || height < 0 || n_devices < 1 || n_devices > RT_MAX_DEVICES)
+        return set_error(RT_ERR_INVALID, "rt_multi_plan_region: bad arguments");
+    *plan = make_multi_plan(*region, width, height, n_devices);
+    return RT_OK;
+}
+
+// Errors of the multi-GPU entries: the reference's render errors, HIP / RCCL errors, bad arguments.
+static int multi_call(rt_camera* cam, const std::function<void()>& f) {
+    if (!cam) return set_error(RT_ERR_INVALID, "null camera");
+    std::lock_guard<std::mutex> lock(cam->mu);
+    try {
+        f();
+        return RT_OK;
+    } catch (const HipError& e) {
+        return set_error(RT_ERR_DEVICE, e.what());
+    } catch (const std::invalid_argument& e) {
+        return set_error(RT_ERR_INVALID, e.what());
+    } catch (const std::exception& e) {
+        return set_error(RT_ERR_RENDER, e.what());
+    }
+}
+
+int rt_camera_render_multi(rt_camera* cam, const int32_t* devices, int32_t n_devices, const rt_region* region,
+                           uint8_t* rgb, float* radiance, rt_render_stats* stats) {
+    if (!region) return set_error(RT_ERR_INVALID, "null region");
+    return multi_call(cam, [&] {
+        unsigned long long m[ST_WORDS];
+        render_multi(cam, devices, n_devices, *region, rgb != nullptr, radiance != nullptr, m,
+                     [&](DevCtx& root) { copy_region_to_host(root, *region, rgb, radiance, root.stream); });
+        DevCtx::stats_from_words(m, stats);
+    });
+}
+
+int rt_camera_render_png_multi(rt_camera* cam, const int32_t* devices, int32_t n_devices, rt_render_stats* stats,
+                               uint8_t** out, size_t* out_len) {
+    if (!out || !out_len) return set_error(RT_ERR_INVALID, "null argument");
+    return multi_call(cam, [&] {
+        const rt_region r{0, 0, cam->build.cam.width, cam->build.cam.height};
+        unsigned long long m[ST_WORDS];
+        DevCtx& root = render_multi(cam, devices, n_devices, r, true, false, m, nullptr);
+        DevCtx::stats_from_words(m, stats);
+        png_out(root, root.stream, out, out_len);
+    });
+}
+
+int rt_camera_multi_info(rt_camera* cam, rt_multi_info* info) {
+    if (!info) return set_error(RT_ERR_INVALID, "null argument");
+    return multi_call(cam, [&] {
+        *info = rt_multi_info{};
+        if (cam->multi.empty()) return;
+        info->n_devices = (int32_t)cam->multi.size();
+        info->transport = cam->multi_transport;
+        info->plan = cam->multi_plan;
+        for (size_t g = 0; g < cam->multi.size(); ++g) {
+            DevCtx& c = *cam->multi[g];
+            info->devices[g] = c.device;
+            c.times(&info->path_ms[g], &info->accum_ms[g]);
+        }
+        DevCtx& root = *cam->multi[0];
+        hip_check(hipEventSynchronize(root.ev_gather1), "hipEventSynchronize");
+        hip_check(hipEventElapsedTime(&info->gather_ms, root.ev_gather0, root.ev_gather1), "hipEventElapsedTime");
+    });
 }
 
 int rt_camera_release_device(rt_camera* cam) {

@@ -5,6 +5,8 @@
  *   createCameraFromSceneData(sceneData, renderOptions)  src/scenes/scenes.ts:60-104
  *   camera.renderRegion(buffer, region) -> RenderStats  src/camera.ts:388-431
  *   generateSceneData(sceneConfig)                      src/scenes/scenes.ts:42-50
+ *   the parallel workers of generateImageBuffer         src/raytracer.ts:60-90,185-205
+ *     (renderRegionMulti, renderPng's gpus: N GPUs from one call, rt_camera_render_multi)
  * through include/rt_amd.h. Errors are thrown as JS Errors carrying the same
  * messages the reference throws (rt_last_error()).
  *
@@ -176,6 +178,81 @@ static napi_value RenderRegion(napi_env env, napi_callback_info info) {
     return stats_object(env, &s);
 }
 
+/* Device ordinals from a JS array of numbers, or 0..n-1 from a number n. Returns the count
+ * (0 and a pending exception on a bad argument). */
+static int32_t get_devices(napi_env env, napi_value v, int32_t* devs) {
+    bool is_arr = false;
+    if (napi_is_array(env, v, &is_arr) != napi_ok) return 0;
+    if (!is_arr) {
+        int32_t n = 0;
+        if (napi_get_value_int32(env, v, &n) != napi_ok || n < 1 || n > RT_MAX_DEVICES) {
+            napi_throw_range_error(env, NULL, "gpus must be 1..16 or an array of device ordinals");
+            return 0;
+        }
+        for (int32_t g = 0; g < n; ++g) devs[g] = g;
+        return n;
+    }
+    uint32_t n = 0;
+    napi_get_array_length(env, v, &n);
+    if (n < 1 || n > RT_MAX_DEVICES) {
+        napi_throw_range_error(env, NULL, "devices must list 1..16 device ordinals");
+        return 0;
+    }
+    for (uint32_t g = 0; g < n; ++g) {
+        napi_value e;
+        if (napi_get_element(env, v, g, &e) != napi_ok || napi_get_value_int32(env, e, &devs[g]) != napi_ok) {
+            napi_throw_type_error(env, NULL, "devices must be numbers");
+            return 0;
+        }
+    }
+    return (int32_t)n;
+}
+
+/* renderRegionMulti(cam, buffer, region, gpus: number | number[]) -> RenderStats: renderRegion
+ * over several GPUs from this one process (rt_camera_render_multi) - the reference's worker
+ * fan-out (src/raytracer.ts:60-90, renderWorker.ts:17-35) with one call: tiles dealt over the
+ * devices, gathered on the first over RCCL, stats merged as RenderStats.merge. */
+static napi_value RenderRegionMulti(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 4) {
+        napi_throw_type_error(env, NULL, "renderRegionMulti(camera, buffer, region, gpus)");
+        return NULL;
+    }
+    rt_camera* cam = get_camera(env, argv[0]);
+    if (!cam) return NULL;
+    bool is_ta = false;
+    CHECK_NAPI(env, napi_is_typedarray(env, argv[1], &is_ta));
+    napi_typedarray_type tt;
+    size_t len = 0, off = 0;
+    void* data = NULL;
+    napi_value ab;
+    if (is_ta) CHECK_NAPI(env, napi_get_typedarray_info(env, argv[1], &tt, &len, &data, &ab, &off));
+    if (!is_ta || (tt != napi_uint8_clamped_array && tt != napi_uint8_array)) {
+        napi_throw_type_error(env, NULL, "buffer must be a Uint8ClampedArray");
+        return NULL;
+    }
+    rt_camera_info ci;
+    if (rt_camera_get_info(cam, &ci)) return throw_rt(env);
+    if (len < (size_t)ci.width * (size_t)ci.height * 3u) {
+        napi_throw_range_error(env, NULL, "buffer is smaller than width*height*3");
+        return NULL;
+    }
+    rt_region r;
+    if (!get_int_prop(env, argv[2], "x", &r.x) || !get_int_prop(env, argv[2], "y", &r.y) ||
+        !get_int_prop(env, argv[2], "width", &r.width) || !get_int_prop(env, argv[2], "height", &r.height)) {
+        napi_throw_type_error(env, NULL, "region must be {x, y, width, height}");
+        return NULL;
+    }
+    int32_t devs[RT_MAX_DEVICES];
+    const int32_t n = get_devices(env, argv[3], devs);
+    if (n == 0) return NULL;
+    rt_render_stats s;
+    if (rt_camera_render_multi(cam, devs, n, &r, (uint8_t*)data, NULL, &s)) return throw_rt(env);
+    return stats_object(env, &s);
+}
+
 /* RenderStats as the reference's object shape (src/render-utils/renderStats.ts:6-19). */
 static napi_value stats_object(napi_env env, const rt_render_stats* sp) {
     const rt_render_stats s = *sp;
@@ -236,26 +313,37 @@ static napi_value EncodePng(napi_env env, napi_callback_info info) {
     return buf;
 }
 
-/* renderPng(camera, bands) -> {png: Buffer, stats}: generateImageBuffer's core
+/* renderPng(camera, bands, gpus?) -> {png: Buffer, stats}: generateImageBuffer's core
  * (src/raytracer.ts:39-113) on the device - `bands` is the reference's worker split
  * (the frame and its merged stats do not depend on it: one launch), the PNG encoded on
- * the GPU (rt_camera_render_png) so only the compressed file crosses PCIe. */
+ * the GPU (rt_camera_render_png) so only the compressed file crosses PCIe. `gpus` (a count
+ * or an array of device ordinals) renders the frame over several GPUs of this process
+ * (rt_camera_render_png_multi). */
 static napi_value RenderPng(napi_env env, napi_callback_info info) {
-    size_t argc = 2;
-    napi_value argv[2];
+    size_t argc = 3;
+    napi_value argv[3];
     CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     if (argc < 1) {
-        napi_throw_type_error(env, NULL, "renderPng(camera, bands)");
+        napi_throw_type_error(env, NULL, "renderPng(camera, bands, gpus?)");
         return NULL;
     }
     rt_camera* cam = get_camera(env, argv[0]);
     if (!cam) return NULL;
     int32_t bands = 1;
     if (argc > 1) CHECK_NAPI(env, napi_get_value_int32(env, argv[1], &bands));
+    int32_t devs[RT_MAX_DEVICES];
+    int32_t ndev = 0;
+    if (argc > 2) {
+        napi_valuetype t;
+        CHECK_NAPI(env, napi_typeof(env, argv[2], &t));
+        if (t != napi_undefined && t != napi_null && (ndev = get_devices(env, argv[2], devs)) == 0) return NULL;
+    }
     uint8_t* png = NULL;
     size_t n = 0;
     rt_render_stats s;
-    if (rt_camera_render_png(cam, bands, &s, &png, &n)) return throw_rt(env);
+    if (ndev > 0 ? rt_camera_render_png_multi(cam, devs, ndev, &s, &png, &n)
+                 : rt_camera_render_png(cam, bands, &s, &png, &n))
+        return throw_rt(env);
     napi_value out, buf;
     CHECK_NAPI(env, napi_create_object(env, &out));
     CHECK_NAPI(env, napi_create_external_buffer(env, n, png, finalize_free, NULL, &buf));
@@ -277,6 +365,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"createCamera", NULL, CreateCamera, NULL, NULL, NULL, napi_default, NULL},
         {"cameraInfo", NULL, CameraInfo, NULL, NULL, NULL, napi_default, NULL},
         {"renderRegion", NULL, RenderRegion, NULL, NULL, NULL, napi_default, NULL},
+        {"renderRegionMulti", NULL, RenderRegionMulti, NULL, NULL, NULL, napi_default, NULL},
         {"encodePng", NULL, EncodePng, NULL, NULL, NULL, napi_default, NULL},
         {"renderPng", NULL, RenderPng, NULL, NULL, NULL, napi_default, NULL},
         {"version", NULL, Version, NULL, NULL, NULL, napi_default, NULL},

@@ -59,6 +59,22 @@ class RtLaunch(C.Structure):
                 ("stream", C.c_void_p), ("synchronize", C.c_int32), ("packed_tiles", C.c_int32)]
 
 
+MAX_DEVICES = 16  # RT_MAX_DEVICES
+GATHER = {0: "rccl", 1: "peer"}  # RT_GATHER_*
+
+
+class RtMultiPlan(C.Structure):
+    _fields_ = [("region", RtRegion), ("n_devices", C.c_int32), ("slab_tiles", C.c_int32), ("tiles", C.c_int64),
+                ("slab_bytes_rgb", C.c_int64), ("slab_bytes_radiance", C.c_int64), ("stats_offset", C.c_int64),
+                ("group_tiles", C.c_int32 * MAX_DEVICES)]
+
+
+class RtMultiInfo(C.Structure):
+    _fields_ = [("n_devices", C.c_int32), ("transport", C.c_int32), ("devices", C.c_int32 * MAX_DEVICES),
+                ("path_ms", C.c_float * MAX_DEVICES), ("accum_ms", C.c_float * MAX_DEVICES),
+                ("gather_ms", C.c_float), ("plan", RtMultiPlan)]
+
+
 class RtError(RuntimeError):
     """An error returned through the C ABI (the reference would throw an Error)."""
 
@@ -108,6 +124,13 @@ _SIGS = {
                                     C.POINTER(C.c_size_t)]),
     "rt_camera_render_png": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(RtRenderStats), C.POINTER(C.c_void_p),
                                        C.POINTER(C.c_size_t)]),
+    "rt_multi_plan_region": (C.c_int, [C.POINTER(RtRegion), C.c_int32, C.c_int32, C.c_int32,
+                                       C.POINTER(RtMultiPlan)]),
+    "rt_camera_render_multi": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.POINTER(RtRegion),
+                                         C.c_void_p, C.c_void_p, C.POINTER(RtRenderStats)]),
+    "rt_camera_render_png_multi": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.POINTER(RtRenderStats),
+                                             C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "rt_camera_multi_info": (C.c_int, [C.c_void_p, C.POINTER(RtMultiInfo)]),
 }
 
 _lib = None
@@ -164,6 +187,17 @@ def check(code: int) -> None:
 def to_json(obj) -> bytes:
     """Serialise like JSON.stringify, keeping Infinity/NaN (accepted by the C parser)."""
     return json.dumps(obj, allow_nan=True, separators=(",", ":")).encode()
+
+
+def multi_plan(region, width: int, height: int, n_devices: int) -> dict:
+    """rt_multi_plan_region: the split of a region over n devices (host only)."""
+    p = RtMultiPlan()
+    reg = RtRegion(*[int(v) for v in region])
+    check(load().rt_multi_plan_region(C.byref(reg), int(width), int(height), int(n_devices), C.byref(p)))
+    return {"region": (p.region.x, p.region.y, p.region.width, p.region.height), "n_devices": p.n_devices,
+            "slab_tiles": p.slab_tiles, "tiles": p.tiles, "slab_bytes_rgb": p.slab_bytes_rgb,
+            "slab_bytes_radiance": p.slab_bytes_radiance, "stats_offset": p.stats_offset,
+            "group_tiles": list(p.group_tiles)[:p.n_devices]}
 
 
 def device_count() -> int:

@@ -157,6 +157,48 @@ class Camera:
         finally:
             self._lib.rt_free(out)
 
+    def render_region_multi(self, buffer, region, devices, radiance=None) -> RenderStats:
+        """Camera.renderRegion over several GPUs from this one process (rt_camera_render_multi):
+        the region's 8x8 tiles dealt round-robin over `devices` (HIP ordinals; one may repeat
+        to rehearse the split on fewer GPUs), gathered on devices[0] over RCCL, stats merged as
+        RenderStats.merge. Same buffers and result as render_region, bit for bit."""
+        ptr, _keep = _host_ptr(buffer, self.byte_length, "buffer")
+        rptr, _keep2 = _host_ptr(radiance, self.byte_length * 4, "radiance")
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        st = _lib.RtRenderStats()
+        reg = _region(region)
+        _lib.check(self._lib.rt_camera_render_multi(self._h, devs, len(devices), C.byref(reg), ptr, rptr, C.byref(st)))
+        return RenderStats._from_c(st)
+
+    def render_multi(self, buffer, devices, radiance=None) -> RenderStats:
+        """Camera.render over several GPUs (render_region_multi of the whole image)."""
+        return self.render_region_multi(buffer, (0, 0, self.image_width, self.image_height), devices, radiance)
+
+    renderRegionMulti = render_region_multi
+
+    def render_png_multi(self, devices):
+        """generateImageBuffer over several GPUs (rt_camera_render_png_multi): the frame gathered on
+        devices[0], PNG encoded there -> (png bytes, merged RenderStats)."""
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        out, n = C.c_void_p(), C.c_size_t()
+        st = _lib.RtRenderStats()
+        _lib.check(self._lib.rt_camera_render_png_multi(self._h, devs, len(devices), C.byref(st), C.byref(out),
+                                                        C.byref(n)))
+        try:
+            return C.string_at(out, n.value), RenderStats._from_c(st)
+        finally:
+            self._lib.rt_free(out)
+
+    def multi_info(self) -> dict:
+        """The last multi-GPU render (rt_camera_multi_info): devices, transport, per-device
+        path / accumulate ms and the root's gather ms (waits for their events)."""
+        i = _lib.RtMultiInfo()
+        _lib.check(self._lib.rt_camera_multi_info(self._h, C.byref(i)))
+        n = i.n_devices
+        return {"n_devices": n, "transport": _lib.GATHER.get(i.transport, "none") if n else "none",
+                "devices": list(i.devices)[:n], "path_ms": list(i.path_ms)[:n], "accum_ms": list(i.accum_ms)[:n],
+                "gather_ms": float(i.gather_ms), "slab_tiles": i.plan.slab_tiles, "tiles": i.plan.tiles}
+
     def render_device(self, *, rgb_ptr=None, radiance_ptr=None, region=None, tile_group=0, tile_groups=1,
                       precision: Optional[str] = None, stream=None, synchronize=False, count_work=False,
                       px_samples_ptr=None, px_bounces_ptr=None, traversal: Optional[str] = None,

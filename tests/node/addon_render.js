@@ -31,7 +31,16 @@ if (mode === 'info') {
   // generateImageBuffer's core on the device: 3 worker bands, PNG encoded on the GPU
   const dev = addon.renderPng(cam, 3);
   fs.writeFileSync(process.argv[4] + '.dev.png', dev.png);
-  console.log(JSON.stringify({ width: info.imageWidth, height: info.imageHeight, stats: [s1, s2], devStats: dev.stats }));
+  // the workers' fan-out as one call over GPUs of this process: device 0 listed 3 times
+  // (the split rehearsed on one GPU), then every visible GPU given as a count
+  const multi = new Uint8ClampedArray(info.imageWidth * info.imageHeight * 3);
+  const sm = addon.renderRegionMulti(cam, multi, { x: 0, y: 0, width: info.imageWidth, height: info.imageHeight },
+                                     [0, 0, 0]);
+  fs.writeFileSync(process.argv[4] + '.multi', Buffer.from(multi.buffer));
+  const devm = addon.renderPng(cam, 1, Number(process.argv[5] || 1));
+  fs.writeFileSync(process.argv[4] + '.multi.png', devm.png);
+  console.log(JSON.stringify({ width: info.imageWidth, height: info.imageHeight, stats: [s1, s2], devStats: dev.stats,
+                               multiStats: sm, multiPngStats: devm.stats }));
 } else if (mode === 'png') {
   // host-only: encodePng of a synthetic frame (no GPU)
   const w = 5, h = 3;

@@ -14,7 +14,7 @@ def test_library_exports_every_declared_symbol(rt):
     assert len(names) >= 20
     for n in sorted(names):
         assert hasattr(lib, n), f"{n} declared in rt_amd.h but not exported"
-    assert lib.rt_version() == 2
+    assert lib.rt_version() == 3
 
 
 def test_build_id_matches_sources(rt):

@@ -60,7 +60,7 @@ def test_addon_render_matches_python_binding(rt, addon, gpu, tmp_path):
     """Two renderRegion calls into one SharedArrayBuffer (the worker split of
     generateImageBuffer) give the library's full-frame image."""
     out_bin = tmp_path / "frame.bin"
-    res = _node(addon, "render", out_bin)
+    res = _node(addon, "render", out_bin, gpu)
     W, H = res["width"], res["height"]
     got = np.frombuffer(out_bin.read_bytes(), np.uint8).reshape(H, W, 3)
     sd = rt.generate_scene_data({"type": "cornell"})
@@ -75,3 +75,8 @@ def test_addon_render_matches_python_binding(rt, addon, gpu, tmp_path):
     assert res["devStats"]["pixels"] == st.pixels and res["devStats"]["samples"]["total"] == st.samples["total"]
     assert sum(s["pixels"] for s in res["stats"]) == st.pixels
     assert sum(s["samples"]["total"] for s in res["stats"]) == st.samples["total"]
+    # renderRegionMulti over [0, 0, 0] and renderPng over every visible GPU: the same frame
+    assert Path(str(out_bin) + ".multi").read_bytes() == ref.tobytes()
+    assert decode_png_rgb(Path(str(out_bin) + ".multi.png").read_bytes()) == (W, H, ref.tobytes())
+    for k in ("multiStats", "multiPngStats"):
+        assert res[k]["pixels"] == st.pixels and res[k]["samples"] == st.samples and res[k]["bounces"] == st.bounces

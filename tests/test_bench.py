@@ -55,3 +55,13 @@ def test_parity_check_accepts_the_oracle_frame_and_flags_one_pixel(rt, oracle):
     other[(j + 1) % 40 if (j + 1) % 40 not in p["rows"] else 0, 0, 0] ^= 1
     r = bench.parity_check(sd, ro, args, other, rgb, rad, st)
     assert not r["ok"] and not r["timed_frame_equals_rerender"]
+
+
+def test_bench_rejects_bad_repeat_counts():
+    """--repeats 0 used to fail with IndexError after the whole warmup."""
+    import bench
+    for bad in (["--repeats", "0"], ["--steps", "0"], ["--warmup", "-1"], ["--gpus", "0"]):
+        with pytest.raises(SystemExit):
+            bench.parse_args(bad)
+    a = bench.parse_args(["--single-process", "--gpus", "2", "--devices", "0,0"])
+    assert a.single_process and a.devices == "0,0"

@@ -260,3 +260,72 @@ def test_render_frame_orders_the_render_stream_after_the_gather_on_every_rank(mo
     names = [c[0] for c in calls]
     assert names == ["render", "stats", "wait", "gather", "wait_for_current"]
     assert calls[-1] == ("wait_for_current", 1234)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 6, 7, 8, 16])
+@pytest.mark.parametrize("W,H,region", [(800, 800, None), (37, 21, None), (64, 64, (3, 2, 59, 61)),
+                                         (1920, 1080, (-5, 100, 700, 2000)), (8, 9, (0, 0, 8, 9)),
+                                         (20, 20, (30, 0, 5, 5))])
+def test_multi_plan_matches_the_tile_split(rt, n, W, H, region):
+    """rt_multi_plan_region (the C ABI's single-process multi-GPU split, rt_camera_render_multi)
+    against the Python restatement bench.py's one-process-per-GPU path uses: the same slab sizes,
+    stats-word offset and per-device tile counts, and every region tile lands in exactly one slab
+    slot that rt_tiles_unpack maps back to it (tile t -> entry t % n, slot t // n)."""
+    from raytracer_amd import _lib
+    from raytracer_amd import distributed as rtd
+    region = region or (0, 0, W, H)
+    p = _lib.multi_plan(region, W, H, n)
+    reg = rtd.clamp_region(region, W, H)
+    assert p["region"] == reg
+    tiles = rtd.tile_count(reg)
+    assert p["tiles"] == tiles and p["n_devices"] == n
+    assert p["slab_tiles"] == rtd.slab_tiles(reg, n)
+    assert p["slab_bytes_rgb"] == rtd.slab_pixels(reg, n) * 3
+    assert p["slab_bytes_radiance"] == p["slab_tiles"] * 64 * 3 * 4
+    assert p["stats_offset"] == p["slab_tiles"] * 64 * 3
+    assert p["stats_offset"] + rtd.STATS_BYTES <= p["slab_bytes_rgb"]
+    assert p["group_tiles"] == [len(rtd.owned_tiles(reg, g, n)) for g in range(n)]
+    assert sum(p["group_tiles"]) == tiles and max(p["group_tiles"] + [0]) <= p["slab_tiles"]
+    seen = set()
+    for g in range(n):
+        for k, t in enumerate(rtd.owned_tiles(reg, g, n)):
+            assert t == g + k * n and k < p["slab_tiles"]  # frame.hip: region tile r + k * groups
+            seen.add(t)
+    assert seen == set(range(tiles))
+
+
+def test_multi_plan_rejects_bad_device_counts(rt):
+    from raytracer_amd import _lib
+    for n in (0, -1, _lib.MAX_DEVICES + 1):
+        with pytest.raises(_lib.RtError):
+            _lib.multi_plan((0, 0, 8, 8), 8, 8, n)
+
+
+def test_multi_stats_merge_matches_renderstats_merge(rt):
+    """The merge rt_camera_render_multi applies to the devices' stats words (merge_stats_words,
+    rt_api.cpp) is RenderStats.merge (renderStats.ts:42-64): restated here over random words and
+    compared with the Python merge bench.py's per-rank path runs (distributed.merge_stats_words)."""
+    import torch
+    from raytracer_amd import distributed as rtd
+    g = np.random.default_rng(7)
+    for n in (1, 2, 5, 8):
+        w = g.integers(0, 1 << 40, size=(n, 8), dtype=np.int64)
+        w[:, 7] = 0
+        w[g.random(n) < 0.3, 2] = -1  # a device without samples: minima ~0
+        w[g.random(n) < 0.3, 5] = -1
+        m = rtd.merge_stats_words(torch.from_numpy(w)).numpy()
+        u = w.astype(np.uint64)
+        assert m[0] == w[:, 0].sum() and m[1] == w[:, 1].sum() and m[4] == w[:, 4].sum()
+        assert np.uint64(m[2]) == u[:, 2].min() and np.uint64(m[5]) == u[:, 5].min()
+        assert m[3] == w[:, 3].max() and m[6] == w[:, 6].max()
+
+
+def test_render_multi_without_a_device_fails_loudly(rt):
+    """No GPU here: the multi-GPU entry returns an error (never a CPU fallback)."""
+    if rt.device_count() > 0:
+        pytest.skip("a device is visible")
+    from raytracer_amd import _lib
+    cam = rt.create_camera_from_scene_data(rt.generate_scene_data({"type": "cornell"}), {"width": 16, "samples": 1})
+    buf = np.zeros((16, 16, 3), np.uint8)
+    with pytest.raises(_lib.RtError):
+        cam.render_multi(buf, [0, 1])

@@ -16,6 +16,7 @@
 #   sections          tools/profile_sections.py (section timers of the chunked / sequential kernels)
 #   poolsections      the same for the pool kernel (variant library 'poolprof': RT_POOL_PROF=1, RT_POOL_K=146)
 #   countexact        tools/count_exact.py (exact tests per ray / per wave-trip)
+#   single            bench.py --single-process (rt_camera_render_multi): N=1, and N=4 on device 0 repeated
 #   bench:<args>      one extra bench line with <args> (underscores become spaces)
 #   ab                runtime-knob A/B (tools/ab_env.sh) over $CFGS x $ARMS (set by the caller:
 #                     lines "tag bench-args" / "arm ENV=V ..."), table in $O/ab/table.txt
@@ -50,6 +51,9 @@ for step in "$@"; do
     fp32) run 200 b_cornell_fp32.log $B --precision fp32 --steps 5 --warmup 1 || exit $? ;;
     adaptive) run 300 b_adaptive.log $B --adaptive --steps 3 --warmup 1 || exit $? ;;
     config5) run 600 b_config5.log $B $CFG5 --steps 1 --warmup 0 --no-count || exit $? ;;
+    single)  # one process, all N GPUs through rt_camera_render_multi (device 0 repeated on a 1-GPU box)
+      run 300 b_single1.log python bench.py --single-process --gpus 1 --no-cpu --steps 10 || exit $?
+      run 300 b_single4.log python bench.py --single-process --gpus 4 --devices 0,0,0,0 --no-cpu --steps 10 || exit $? ;;
     bench:*) a=${step#bench:}; run 300 b_extra_$(echo $a | tr -c 'a-z0-9' _ | cut -c1-40).log $B ${a//_/ } || exit $? ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
