@@ -228,7 +228,15 @@ def roofline(cfg_key: str, build: str, samples: int, kernel_ms: float, counters,
     if v:
         ips = v["valu_insts_per_sample"] / 64.0  # wave instructions per sample
         ach = ips * samples / k_s / 1e9
+        # issue-weighted: an f64 add / mul / fma issues at half the f32 rate on gfx950
+        # (78.6 vs 157.3 TFLOP/s) and a transcendental at a quarter, so those instructions hold
+        # the SIMD 2x / 4x as long as `frac` counts them (mix: their shares of SQ_INSTS_VALU)
+        mix = v.get("mix", {})
+        w = (1.0 + sum(mix.get(k, 0.0) for k in ("add_f64", "mul_f64", "fma_f64"))
+             + 3.0 * (mix.get("trans_f32", 0.0) + mix.get("trans_f64", 0.0)))
         out.update({"achieved": round(ach, 2), "frac": round(ach / VALU_PEAK_GINST, 4),
+                    "frac_issue_weighted": round(ach * w / VALU_PEAK_GINST, 4),
+                    "issue_weights": {"f64_add_mul_fma": 2, "transcendental": 4, "factor": round(w, 4)},
                     "lane_util": v["lane_util"], "useful_lane_frac": round(ach / VALU_PEAK_GINST * v["lane_util"], 4),
                     "valu_wave_insts_per_sample": round(ips, 2),
                     "pmc_kernel": v["kernel"], "pmc_build": v.get("build_id"), "pmc_stale": v.get("build_id") != build,

@@ -23,9 +23,8 @@ struct LaunchGeom {
 
 // LDS budget (stack + [tnodes][prims]) up to which the scene is copied into LDS.
 constexpr int kLdsSceneMaxBytes = 152 * 1024;
-// Static LDS of the chunked / pool kernels (the phase table; with RT_COOP_LEAF the per-wave
-// segment-start tables, 128 bytes per wave), beside the dynamic allocation.
-constexpr size_t kStaticLdsBytes = 512 + (RT_COOP_LEAF ? (size_t)(kBlockChunk / kWave) * kWave * 2 : 0);
+// Static LDS of the chunked / pool kernels (the phase table), beside the dynamic allocation.
+constexpr size_t kStaticLdsBytes = 512;
 // ... plus the per-wave section timers of the diagnostic variants: every kernel of a
 // count == 2 launch, and every pool kernel of an RT_POOL_PROF build.
 inline size_t static_lds_bytes(int count, bool pool) {
@@ -73,11 +72,10 @@ hipError_t launch_tiles_unpack(const void* slabs, int groups, int slab_tiles, co
 // (StackT, pt_kernel.hpp)
 inline size_t stack_lds_bytes(int stack_depth, int trav, int n_prims, bool lds_tree = false) {
     if (trav == TRAV_BRUTE)  // larger forced brute-force scenes take the in-order loop (no LDS)
-        return RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims ? (size_t)std::max(n_prims, 1) * kStackStride * sizeof(uint16_t)
-                                                           : 0;
+        return n_prims <= kBruteMaxPrims ? (size_t)std::max(n_prims, 1) * kStackStride * sizeof(uint16_t) : 0;
     const size_t d = (size_t)(stack_depth > 0 ? stack_depth : 1);
     const size_t e = lds_tree ? sizeof(StackT<1>) : sizeof(StackT<0>);
-    return d * kStackStride * ((trav == TRAV_FAST && kStackTnear) ? 2 * e : e);
+    return d * kStackStride * e;
 }
 
 // The kernel template instance of a launch (one per scalar precision unit: pt_ref.hip,

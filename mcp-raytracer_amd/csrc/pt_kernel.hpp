@@ -65,10 +65,8 @@ struct DevScene {
     int32_t n_top;                      // launches walking the tree from global memory: nodes [0, n_top)
                                         // (breadth-first: the tree's top) have a padded copy in LDS
     const char* top_lds;                // ... after the traversal stack (scene_view; LDSS 0 only)
-    const RtQ4Node* __restrict__ qnodes; // the tree's compressed 4-wide nodes (global), or null
     const RtLeafSph* __restrict__ tsph2; // trees walked from global memory: leaf-order sphere records with
                                          // the fp64 radius and the slot (one load per exact test), or null
-    int32_t qtree;                      // LDSS 0 launch walking qnodes (and caching their top in LDS)
     int32_t nearfar;                    // 4-wide node step picks near / far rows by the ray's signs (t4_step);
                                         // scene_view sets a constant per LDS level (see there)
     int32_t troot;                      // fast traversal root reference
@@ -137,42 +135,21 @@ enum Traversal : int32_t { TRAV_FAST = 0, TRAV_REFERENCE = 1, TRAV_BRUTE = 2, TR
 constexpr bool trav_fast(int t) { return t == TRAV_FAST || t == TRAV_FAST_DEFER; }
 constexpr int kBruteMaxPrims = 16;  // AUTO picks BRUTE up to this many primitives (nearest-first form: <= 32)
 
-// Minimum waves per SIMD the path kernel is register-allocated for
-// (__launch_bounds__ second argument): 3 => <= 168 VGPRs.
-#ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 3
-#endif
-
 constexpr int kWave = 64;
 // Persistent workgroups, one per CU, sharing one LDS scene copy:
 //   sequential kernel 768 threads (12 waves = 3 per SIMD, <= 168 VGPRs),
-//   chunked kernel RT_CHUNK_BLOCK threads (1024: 16 waves = 4 per SIMD, <= 128 VGPRs).
-#ifndef RT_CHUNK_BLOCK
-#define RT_CHUNK_BLOCK 1024
-#endif
-#ifndef RT_SEQ_BLOCK
-#define RT_SEQ_BLOCK 768
-#endif
-constexpr int kBlock = RT_SEQ_BLOCK;
-constexpr int kBlockChunk = RT_CHUNK_BLOCK;
+//   chunked kernel 1024 threads (16 waves = 4 per SIMD, <= 128 VGPRs).
+constexpr int kBlock = 768;
+constexpr int kBlockChunk = 1024;
 constexpr int kStackStride = 1024;  // LDS traversal-stack column stride (>= any block size)
-// Stack entries of the fast walk (RT_STK16): 16-bit in launches whose tree is LDS-resident (its
+// Stack entries of the fast walk: 16-bit in launches whose tree is LDS-resident (its
 // node references and leaf codes ~(first << 3 | count) fit an int16: at most ~1,000 nodes and
 // primitives fit the LDS copy), so the stack takes half the LDS and the material / light tables
 // fit beside it (LDS residency level 2); 32-bit where the tree is walked from global memory.
-#ifndef RT_STK16
-#define RT_STK16 1
-#endif
+// Entries hold a node reference only (a popped subtree is culled one level later by its
+// children's slab tests).
 template <int LDSS>
-using StackT = typename std::conditional<(LDSS > 0 && RT_STK16 != 0), int16_t, int32_t>::type;
-// Fast traversal stack entries: node reference only (4 B; a popped subtree is
-// culled one level later by its children's slab tests), or also its entry
-// distance (8 B; culled on pop). 4 B keeps deeper SAH trees LDS-resident.
-#ifndef RT_STACK_TNEAR
-#define RT_STACK_TNEAR 0
-#endif
-constexpr bool kStackTnear = RT_STACK_TNEAR != 0;
-static_assert(!(RT_BVH4 && RT_STACK_TNEAR), "the 4-wide traversal keeps 4-byte stack entries");
+using StackT = typename std::conditional<(LDSS > 0), int16_t, int32_t>::type;
 constexpr int kTile = 8;          // 8x8 pixels per wave-tile
 constexpr int kEmitStack = 128;   // emission terms kept for the right fold (EMIT builds)
 
@@ -204,23 +181,14 @@ __device__ __forceinline__ double m_cos(double x) { return ::cos(x); }
 __device__ __forceinline__ float m_cos(float x) { return ::cosf(x); }
 __device__ __forceinline__ double m_sin(double x) { return ::sin(x); }
 __device__ __forceinline__ float m_sin(float x) { return ::sinf(x); }
-// Math.cos(x) and Math.sin(x) of one argument. RT_SINCOS=1 (default): ocml's sincos
-// evaluates the sine and cosine polynomials once (separate sin + cos calls each
-// evaluate both and select) and returns bit-for-bit sin(x) and cos(x)
-// (tools/probes/sincos_check: all 2^32 cosine-PDF angles, fp64 and fp32).
-// Cornell 7718 -> 7933 Msamples/s (profiles/r01/sincos/).
-#ifndef RT_SINCOS
-#define RT_SINCOS 1
-#endif
+// Math.cos(x) and Math.sin(x) of one argument: ocml's sincos evaluates the sine and cosine
+// polynomials once (separate sin + cos calls each evaluate both and select) and returns
+// bit-for-bit sin(x) and cos(x) (tools/probes/sincos_check: all 2^32 cosine-PDF angles, fp64
+// and fp32). Cornell 7718 -> 7933 Msamples/s (profiles/r01/sincos/).
 template <class Real>
 __device__ __forceinline__ void m_sincos(Real x, Real& s, Real& c) {
-#if RT_SINCOS
     if constexpr (sizeof(Real) == 8) ::sincos(x, &s, &c);
     else ::sincosf(x, &s, &c);
-#else
-    c = m_cos(x);
-    s = m_sin(x);
-#endif
 }
 // Math.pow(x, 5) of Schlick's approximation (src/materials/dielectric.ts:98),
 // correctly rounded: x^5 in double-double (exact x^2 and x^4 products via FMA),
@@ -239,13 +207,9 @@ __device__ __forceinline__ float pow5(float x) {
 }
 __device__ __forceinline__ double m_abs(double x) { return ::fabs(x); }
 __device__ __forceinline__ float m_abs(float x) { return ::fabsf(x); }
-// Math.sqrt: rt_math.hpp sqrt_rn wherever no range scaling applies (x >= 2^-767 or +inf / NaN: a
-// high word >= 0x10000000 as a signed integer, one compare), else the general expansion - the same
-// bits for every x.
-__device__ __forceinline__ double m_sqrt(double x) {
-    if ((RT_FP64_SHORT & 2) && (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32) >= 0x10000000) return sqrt_rn(x);
-    return ::sqrt(x);
-}
+// Math.sqrt. (Routing it through rt_math.hpp sqrt_rn behind a range test was no faster anywhere:
+// the branch costs what the skipped scaling steps save, profiles/r04/fp64/.)
+__device__ __forceinline__ double m_sqrt(double x) { return ::sqrt(x); }
 __device__ __forceinline__ float m_sqrt(float x) { return ::sqrtf(x); }
 
 template <class Real> struct K {
@@ -398,17 +362,7 @@ constexpr float kRel = 1e-5f;
 // still bounds it. The one changed form is the slab test, which no longer subtracts first
 // (see slab_t4 / FRay::eps). Before: SQ_INSTS_VALU_FMA_F32 was 0.0 % of VALU
 // on Cornell ref, 1.0 % on spheres-500 and 0.5 % on spheres-100k.
-#ifndef RT_FUSED_FILTERS
-#define RT_FUSED_FILTERS 1
-#endif
-#ifndef RT_NEARFAR
-#define RT_NEARFAR 1  // 0: rows in node order, near / far planes by min / max (A/B)
-#endif
-#if RT_FUSED_FILTERS
 #define RT_FP32_FUSED _Pragma("clang fp contract(fast)")
-#else
-#define RT_FP32_FUSED
-#endif
 
 // Axis-aligned quad (scene.cpp encode_axis_quad): Plane.intersect + Quad's
 // alpha/beta test with the terms that are exact zeros dropped. Every kept
@@ -651,7 +605,7 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
         // |t_a| = |b - o_a| |inv_a| >= 0.75 |o_a inv_a| and the error is relative, <= 2.7u |t_a|,
         // inside slab_accept's relative 2e-6 (~33u) with the rcp and fma roundings (~3u).
         m = ::fabsf(c) >= 1e-3f * dmax ? ::fmaxf(m, an) : m;
-        f.nrow[a] = 16 * a + (RT_NEARFAR && f.inv[a] < 0.0f ? 48 : 0);
+        f.nrow[a] = 16 * a + (f.inv[a] < 0.0f ? 48 : 0);
     }
     // 1e-6 * max|o * inv| ~ 16 u: covers the rounding of o * inv at both ends of the interval
     f.eps = m * 1e-6f;
@@ -712,16 +666,10 @@ __device__ __forceinline__ bool slab(const RtNode& n, const R& f, float thi, flo
 // in LDS beside the stack (t4_step reads a node from there or from global memory: two loads in two
 // branches, so each stays a ds_read / global_load - one generic pointer made them flat loads,
 // 3.5 % slower on spheres-100k).
-#ifndef RT_UMUL24
-#define RT_UMUL24 1
-#endif
+// (a 24-bit multiply, full rate: node indices stay below 2^24, scene.cpp make_t4nodes)
 __device__ __forceinline__ const RtT4Node* t4_node(const DevScene& S, int ref) {
-#if RT_UMUL24  // (a 24-bit multiply, full rate: node indices stay below 2^24, scene.cpp make_t4nodes)
     return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) +
                                              (size_t)__umul24((unsigned)ref, (unsigned)S.t4_stride));
-#else
-    return reinterpret_cast<const RtT4Node*>(reinterpret_cast<const char*>(S.tnodes) + (size_t)ref * S.t4_stride);
-#endif
 }
 struct T4Rows {
     float4 nr[3], fr[3];  // per axis: the four children's near-plane / far-plane coordinates
@@ -786,59 +734,10 @@ __device__ __forceinline__ int t4_push(uint32_t (&k)[4], int (&r)[4], int n, SK*
     return next;
 }
 
-// One step of the 4-wide walk over compressed nodes (RtQ4Node; LDSS 0 launches with S.qtree):
-// the same slab test and push order as t4_step on boxes decoded exactly from the 8-bit grid
-// (fma(q, scl, org) is exact by construction, scene.cpp make_q4nodes) - boxes that contain the
-// 128-byte node's, so the walk stays conservative and the (t, slot) minimum unchanged. Half the
-// bytes per node: 4 row loads instead of 7, and twice the nodes in the LDS top cache (80-byte
-// stride there: 20 i + 4 r covers 16 bank windows for i mod 16).
-constexpr int kQ4LdsStride = (int)sizeof(RtQ4Node) + 16;
-template <int STRIDE, class SK>
-__device__ __forceinline__ int q4_step(const DevScene& S, int ref, const FRay& f, float thi, SK* stk, int& sp) {
-    typedef float v4 __attribute__((ext_vector_type(4)));
-    v4 h0, h1, h2, h3;
-    if (ref < S.n_top) {
-        typedef const __attribute__((address_space(3))) v4* P4;
-        const P4 b = (P4)__builtin_assume_aligned(S.top_lds + (size_t)ref * kQ4LdsStride, 16);
-        h0 = b[0]; h1 = b[1]; h2 = b[2]; h3 = b[3];
-    } else {
-        typedef const __attribute__((address_space(1))) v4* P4;
-        const P4 b = (P4)__builtin_assume_aligned(S.qnodes + ref, 16);
-        h0 = b[0]; h1 = b[1]; h2 = b[2]; h3 = b[3];
-    }
-    const float org[3] = {h0.x, h0.y, h0.z};
-    const float scl[3] = {h0.w, h1.x, h1.y};
-    const uint32_t qlo[3] = {__float_as_uint(h1.z), __float_as_uint(h1.w), __float_as_uint(h2.x)};
-    const uint32_t qhi[3] = {__float_as_uint(h2.y), __float_as_uint(h2.z), __float_as_uint(h2.w)};
-    const int cr[4] = {__float_as_int(h3.x), __float_as_int(h3.y), __float_as_int(h3.z), __float_as_int(h3.w)};
-    uint32_t k[4];
-    int r[4];
-    int n = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        float tn = kTminLo, tf = thi;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float lo = __builtin_fmaf((float)((qlo[a] >> (8 * c)) & 255u), scl[a], org[a]);
-            const float hi = __builtin_fmaf((float)((qhi[a] >> (8 * c)) & 255u), scl[a], org[a]);
-            const float t0 = slab_t(lo, f, a);
-            const float t1 = slab_t(hi, f, a);
-            tn = ::fmaxf(tn, ::fminf(t0, t1));
-            tf = ::fminf(tf, ::fmaxf(t0, t1));
-        }
-        const bool hit = (cr[c] != kT4Empty) & slab_accept(tn, tf, f);
-        k[c] = hit ? __float_as_uint(tn) : ~0u;
-        r[c] = cr[c];
-        n += hit ? 1 : 0;
-    }
-    return t4_push<STRIDE>(k, r, n, stk, sp);
-}
-
 template <int STRIDE, class SK>
 __device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f, float thi, SK* stk, int& sp) {
-    if (S.qtree) return q4_step<STRIDE>(S, ref, f, thi, stk, sp);
     T4Rows R;
-    const bool nf = RT_NEARFAR && S.nearfar;
+    const bool nf = S.nearfar;
     if (ref < S.n_top) t4_rows<3>(S.top_lds + (size_t)ref * (sizeof(RtT4Node) + 16), f, nf, R);
     else if (S.n_top > 0) t4_rows<1>(t4_node(S, ref), f, nf, R);  // (LDSS 0: the rest is in global memory)
     else t4_rows<0>(t4_node(S, ref), f, nf, R);
@@ -1014,21 +913,18 @@ __device__ __forceinline__ float upper_f(Real t) {
     return x + ::fabsf(x) * 4e-6f + 1e-30f;
 }
 
-// `stk` / `stkt`: this lane's columns of the LDS node / entry-distance stacks.
+// `stk`: this lane's column of the LDS node stack.
 // Walks the children-in-parent tree (RtTNode): one 64-byte node read tests
 // both children; the nearer hit child is taken, the farther pushed (with its
 // entry distance when kStackTnear, culled on pop against the best hit).
 //
-// Lanes of a wave reach leaves at different steps. RT_TRAV_WW (default) runs
-// node steps and leaf tests as two separate loops: a lane that reaches a leaf
+// Lanes of a wave reach leaves at different steps. Node steps and leaf tests run as two
+// separate loops: a lane that reaches a leaf
 // parks it and keeps walking nodes until every lane still walking holds a
 // parked leaf, then the wave tests leaves together - otherwise nearly every
 // node step would also pay for some lane's (four times longer) leaf test.
 // Node steps taken while a leaf is parked cull with a possibly stale bound;
 // that only costs extra node tests (the answer is the (t, slot) minimum).
-#ifndef RT_TRAV_WW
-#define RT_TRAV_WW 1
-#endif
 constexpr int kTravDone = (int)0x80000000;  // no node / leaf (leaf refs are ~v, v < 2^31 - 1)
 
 // Deferred exact sphere tests (DEFER, TRAV_FAST_DEFER kernels): a leaf's sphere that passes the
@@ -1057,16 +953,12 @@ __device__ __forceinline__ void resolve_pending(const DevScene& S, const RayK<Re
 }
 
 // A leaf's primitives in leaf order: the fp32 pre-filter from the compact leaf-order record, then
-// the exact test (or, with DEFER, the pending-candidate rule). L2 (trees walked from global memory,
-// RT_TSPH2): one 32-byte record per primitive (S.tsph2) that also carries the fp64 radius and the
+// the exact test (or, with DEFER, the pending-candidate rule). L2 (trees walked from global memory):
+// one 32-byte record per primitive (S.tsph2) that also carries the fp64 radius and the
 // slot, so a sphere's exact test needs no dependent tprims -> RtPrim loads (two L2 round trips).
-// (Round 5 also tried loading a leaf's four records before its first test: spheres-100k
-// 37.1 -> 44.8 ms, spheres-500 +0 %, profiles/r05/coop_v2_prefetch/ - dropped.)
-#ifndef RT_TSPH2
-#define RT_TSPH2 1
-#endif
-// (Also tried: loading a parked leaf's record when it is parked, so the load overlaps the rest of
-// the node loop - spheres-100k 30.0 -> 36.0 ms, profiles/r05/leaf_pre/.)
+// (Round 5 also tried loading a leaf's four records before its first test, and loading a
+// parked leaf's record when it is parked: spheres-100k 37.1 -> 44.8 and 30.0 -> 36.0 ms,
+// profiles/r05/coop_v2_prefetch/, leaf_pre/ - dropped.)
 template <class Real, bool COUNT, bool DEFER, bool L2 = false>
 __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK<Real>& r, const FRay& f, float& thi,
                                           Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt) {
@@ -1136,7 +1028,7 @@ __device__ __forceinline__ void leaf_test(const DevScene& S, int ref, const RayK
 
 template <class Real, bool COUNT, bool DEFER, class SK>
 __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Real>& r, Real& t_hit, SK* stk,
-                                                float* stkt, uint32_t* cnt) {
+                                                uint32_t* cnt) {
     const FRay f = make_fray(r.o, r.d);
     Real best_t = (Real)__builtin_inf();
     int best = -1;
@@ -1152,40 +1044,19 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
     int sp = 0;
     // next stacked entry (kTravDone when the stack is empty)
     auto pop = [&]() -> int {
-        while (sp > 0) {
+        if (sp > 0) {
             --sp;
-            if (!kStackTnear || stkt[sp * kStackStride] <= thi) return stk[sp * kStackStride];
+            return stk[sp * kStackStride];
         }
         return kTravDone;
     };
-#if RT_BVH4
     // one 4-wide node step: the nearest hit child is next, the other hit
     // children are pushed farthest first (so the nearer pop first)
     auto node_step = [&](int ref) -> int {
         if (COUNT) cnt[CT_NODE] += 4;
         return t4_step<kStackStride>(S, ref, f, thi, stk, sp);
     };
-#else
-    // one node step: the next node / leaf to visit
-    auto node_step = [&](int ref) -> int {
-        const RtTNode nd = S.tnodes[ref];
-        float ta, tb;
-        if (COUNT) cnt[CT_NODE] += 2;
-        const bool ha = slab(nd.box[0], f, thi, ta);
-        const bool hb = slab(nd.box[1], f, thi, tb);
-        if (ha && hb) {
-            const bool a_first = ta <= tb;
-            stk[sp * kStackStride] = (SK)(a_first ? nd.box[1].a : nd.box[0].a);
-            if (kStackTnear) stkt[sp * kStackStride] = a_first ? tb : ta;
-            ++sp;
-            return a_first ? nd.box[0].a : nd.box[1].a;
-        }
-        if (ha || hb) return ha ? nd.box[0].a : nd.box[1].a;
-        return pop();
-    };
-#endif
     int ref = S.troot;
-#if RT_TRAV_WW
     int leaf = kTravDone;  // parked leaf
     while (ref != kTravDone || leaf != kTravDone) {
         while (ref >= 0) {
@@ -1209,23 +1080,13 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
             }
         }
     }
-#else
-    while (ref != kTravDone) {
-        if (ref < 0) {
-            leaf_test<Real, COUNT, DEFER>(S, ref, r, f, thi, best_t, best, pk, plo, cnt);
-            ref = pop();
-        } else {
-            ref = node_step(ref);
-        }
-    }
-#endif
     resolve_pending<Real, COUNT>(S, r, thi, best_t, best, pk, cnt);  // the whole wave at once
     t_hit = best_t;
     return best;
 }
 
 // ---------------------------------------------------------------------------
-// Resumable fast traversal (chunked kernel, RT_RESUME). closest_hit_fast keeps
+// Resumable fast traversal (chunked kernel). closest_hit_fast keeps
 // the whole wave in its loop until the lane with the longest walk is done - a
 // ray grazing a field of spheres can need ten times the mean node visits, and
 // every other lane idles meanwhile. Here a lane's walk state persists across
@@ -1234,12 +1095,6 @@ __device__ __forceinline__ int closest_hit_fast(const DevScene& S, const RayK<Re
 // to them. Same walk (culling, parked leaves, (t, slot) minimum) as
 // closest_hit_fast, so the same hit.
 // ---------------------------------------------------------------------------
-#ifndef RT_RESUME
-#define RT_RESUME 1
-#endif
-#ifndef RT_WALK_LEAVES
-#define RT_WALK_LEAVES 1  // leaves a walking lane parks before it idles in the node loop (1 or 2)
-#endif
 template <class Real>
 struct FastWalk {
     int ref, leaf, sp, best;
@@ -1263,151 +1118,6 @@ __device__ __forceinline__ void fast_walk_begin(const DevScene& S, V3 o, V3 d, F
     W.ref = slab(S.root_box, f, W.thi, tn0) ? S.troot : kTravDone;
 }
 
-// ---------------------------------------------------------------------------
-// Cooperative leaf phase (RT_COOP_LEAF): the leaf tests of a round, flattened over the wave.
-// In the parked-leaf walk each lane tests its own leaf's 1-7 primitives in turn, so a leaf
-// phase issues the fp32 pre-filter max(count) times at the lanes that hold a leaf (spheres-500:
-// 20.5 of 64 lanes per leaf test, round-4 sections.log). Here every (lane, primitive) pair of
-// the wave's parked leaves gets its own lane:
-//  * ballots of the bits of each lane's pair count give its exclusive prefix (mbcnt) and the
-//    wave's total; in each window of 64 pairs every owner marks its first pair's position in a
-//    128-byte per-wave LDS table, a ballot of the marks and a count-leading-zeros give each pair
-//    lane its segment's start, and one ds_bpermute from there its owner;
-//  * the pair lane fetches the owner's ray, leaf codes and current bound with ds_bpermute,
-//    loads the primitive's compact record and runs the fp32 pre-filter (sphere_maybe[_hi]);
-//  * each owner then reads back, with ds_bpermute, only the pairs that passed (a ballot mask,
-//    ascending = the leaf's primitive order), and applies exactly the sequential leaf_test rules (the pending-candidate
-//    rule of DEFER, or the exact fp64 test) with its CURRENT bound: a pair pre-filtered against
-//    the owner's older (larger) bound passes the current test iff lo <= the current bound,
-//    since lo and hi do not depend on the bound. Non-sphere primitives go to the owner's
-//    prim_candidate unchanged. So the (t, slot) minimum - the hit - is the sequential one.
-// bsrc: wave-uniform control flow only (every lane executes the bpermutes).
-// ---------------------------------------------------------------------------
-#ifndef RT_COOP_LEAF
-#define RT_COOP_LEAF 0
-#endif
-constexpr int kCoopNonSphere = 0x40000000;  // pair slot flag: not a sphere (the owner decides exactly)
-__device__ __forceinline__ int lane_prefix(unsigned long long m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ int bperm_i(int src, int v) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
-__device__ __forceinline__ float bperm_f(int src, float v) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
-}
-// The fields of FRay the sphere pre-filter reads (o, d, a, ia, dn), as make_fray computes them.
-__device__ __forceinline__ FRay fray_sphere(float ox, float oy, float oz, float dx, float dy, float dz) {
-    RT_FP32_FUSED
-    FRay f;
-    f.o[0] = ox; f.o[1] = oy; f.o[2] = oz;
-    f.d[0] = dx; f.d[1] = dy; f.d[2] = dz;
-    f.a = dx * dx + dy * dy + dz * dz;
-    f.ia = __builtin_amdgcn_rcpf(f.a);
-    f.dn = __builtin_amdgcn_sqrtf(f.a) * (1.0f + kRel);
-    return f;
-}
-
-template <class Real, bool COUNT, bool DEFER, bool PROF>
-__device__ __forceinline__ void coop_leaves(const DevScene& S, const FRay& f, const RayK<Real>& r, int la, int lb,
-                                            float& thi, Real& best_t, int& best, int& pk, float& plo, uint32_t* cnt,
-                                            uint16_t* tab, Prof* pf) {
-    const int lane = (int)(threadIdx.x & (kWave - 1));
-    const int va = la != kTravDone ? ~la : 0;  // leaf code (first << 3 | count)
-    const int vb = lb != kTravDone ? ~lb : 0;
-    const int c = (va & 7) + (vb & 7);         // this lane's pairs, <= 14
-    int ex = 0, total = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const unsigned long long m = __ballot((c >> b) & 1);
-        ex += lane_prefix(m) << b;
-        total += __popcll(m) << b;
-    }
-    const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
-    for (int base = 0; base < total; base += kWave) {  // (total: wave-uniform)
-        // window [base, base + 64) of the pair sequence: each owner whose pairs reach into it
-        // marks its first pair's position with (lane + 1, pairs before the window)
-        const int p0 = ex - base;
-        const bool in = c > 0 && p0 + c > 0 && p0 < kWave;
-        const int dst = max(p0, 0);
-        tab[lane] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (in) tab[dst] = (uint16_t)((lane + 1) | (max(-p0, 0) << 8));
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const int sv = tab[lane];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const unsigned long long starts = __ballot(sv != 0);
-        const unsigned long long below = starts & le;
-        const int sp0 = below ? 63 - __builtin_clzll(below) : 0;  // the nearest segment start at or below
-        const int so = bperm_i(sp0, sv);
-        const bool act = base + lane < total;
-        const int o = act ? (so & 0xff) - 1 : lane;
-        const int k = lane - sp0 + (so >> 8);  // pair index within the owner's leaves
-        const int va_o = bperm_i(o, va), vb_o = bperm_i(o, vb);
-        const float thi_o = bperm_f(o, thi);
-        const FRay fo = fray_sphere(bperm_f(o, f.o[0]), bperm_f(o, f.o[1]), bperm_f(o, f.o[2]), bperm_f(o, f.d[0]),
-                                    bperm_f(o, f.d[1]), bperm_f(o, f.d[2]));
-        float lo = __builtin_inff(), hi = __builtin_inff();
-        int slot = 0;
-        bool keep = false;  // the owner must look at this pair
-        if (act) {
-            if (PROF) pcount<PROF>(*pf, PR_LEAF);
-            const int ca_o = va_o & 7;
-            const int m = k < ca_o ? (va_o >> 3) + k : (vb_o >> 3) + (k - ca_o);
-            const float4 g = S.tsph[m];
-            slot = S.tprims[m];
-            if (g.w == g.w) {
-                if (COUNT) cnt[CT_SPHERE]++;
-                float l, h = __builtin_inff();
-                keep = DEFER ? sphere_maybe_hi(g, fo, thi_o, l, h) : sphere_maybe(g, fo, thi_o, l);
-                lo = l;
-                hi = h;
-            } else {
-                keep = true;  // not a sphere: the owner decides exactly (prim_candidate)
-                slot |= kCoopNonSphere;
-            }
-        }
-        // owners: the pairs they must look at, in the leaves' primitive order (ascending position)
-        const unsigned long long kept = __ballot(keep);
-        const int n_in = in ? min(p0 + c, kWave) - dst : 0;
-        unsigned long long cm = in ? (kept >> dst) & (n_in >= 64 ? ~0ull : ((1ull << n_in) - 1ull)) : 0ull;
-        while (__ballot(cm != 0ull) != 0ull) {
-            const int pos = cm ? dst + __builtin_ctzll(cm) : lane;
-            const float lk = bperm_f(pos, lo), hk = bperm_f(pos, hi);
-            const int sk = bperm_i(pos, slot);
-            if (cm) {
-                cm &= cm - 1ull;
-                if (sk & kCoopNonSphere) {
-                    const int ks = sk & ~kCoopNonSphere;
-                    Real t;
-                    if (prim_candidate<Real, COUNT>(S.prims[ks], ray_at_use<Real>(r), f, thi, t, cnt) &&
-                        (t < best_t || (t == best_t && ks < best))) {
-                        best_t = t;
-                        best = ks;
-                        thi = ::fminf(thi, upper_f<Real>(t));
-                    }
-                } else if (lk <= thi) {  // passes sphere_maybe[_hi] at the current bound
-                    if constexpr (DEFER) {
-                        if (pk >= 0 && !(hk < plo)) resolve_pending<Real, COUNT>(S, r, thi, best_t, best, pk, cnt);
-                        if (lk <= thi) {
-                            pk = sk;
-                            plo = lk;
-                            thi = ::fminf(thi, hk);
-                        }
-                    } else {
-                        if (COUNT) count_exact(cnt);
-                        Real t;
-                        if (sphere_t<Real>(S.prims[sk], ray_at_use<Real>(r), K<Real>::TMIN, (Real)__builtin_inf(), t) &&
-                            (t < best_t || (t == best_t && sk < best))) {
-                            best_t = t;
-                            best = sk;
-                            thi = ::fminf(thi, upper_f<Real>(t));
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
 // Called by the whole wave with uniform control flow; lanes with `walking`
 // advance their walks. Returns when no lane walks, or (unless `drain`) after at
 // least one round once `min_ready` lanes of the wave are not walking.
@@ -1417,62 +1127,12 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                                                  SK* stk, int min_ready, bool drain, uint32_t* cnt, Prof* pf = nullptr) {
     const FRay f = make_fray(o, d);
     const RayK<Real> r = make_ray<Real>(o, d);
-    float* stkt = nullptr;
-    (void)stkt;
     int rounds = 0;
-#if RT_COOP_LEAF
-    __shared__ uint16_t coop_tab[kBlockChunk / kWave][kWave];
-    uint16_t* tab = coop_tab[threadIdx.x / kWave];
-#endif
     while (true) {
         const unsigned long long wm = __ballot(walking);
         if (wm == 0ull) break;
         if (rounds > 0 && !drain && kWave - __popcll(wm) >= min_ready) break;
         ++rounds;
-#if RT_COOP_LEAF
-        int ref = W.ref, leaf = W.leaf, leaf2 = kTravDone;
-        int sp = W.sp;
-        float thi = W.thi;
-        auto pop = [&]() -> int {
-            if (sp > 0) {
-                --sp;
-                return stk[sp * STRIDE];
-            }
-            return kTravDone;
-        };
-        if (walking) {
-            while (ref >= 0) {
-                if (PROF) pcount<PROF>(*pf, PR_NODE);
-                if (COUNT) cnt[CT_NODE] += 4;
-                ref = t4_step<STRIDE>(S, ref, f, thi, stk, sp);
-                if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
-                    leaf = ref;
-                    ref = pop();
-                }
-                if (__ballot(leaf == kTravDone) == 0ull) break;  // every walking lane holds a leaf
-            }
-            if (PROF) psec<PROF>(*pf, PR_WNODE);
-            if (leaf == kTravDone && ref != kTravDone) {
-                leaf = ref;
-                ref = pop();
-            }
-            if (ref < 0 && ref != kTravDone) {  // the walk also stopped on a leaf: test it too
-                leaf2 = ref;
-                ref = pop();
-            }
-        }
-        coop_leaves<Real, COUNT, DEFER, PROF>(S, f, r, leaf, leaf2, thi, W.best_t, W.best, W.pk, W.plo, cnt, tab, pf);
-        if (PROF) psec<PROF>(*pf, PR_WLEAF);
-        if (walking) {
-            // a leaf popped last stays in W.ref: the next round's leaf phase takes it
-            W.ref = ref;
-            W.leaf = kTravDone;
-            W.sp = sp;
-            W.thi = thi;
-            if (ref == kTravDone) walking = false;
-        }
-        continue;
-#endif
         if (walking) {
             int sp = W.sp;
             float thi = W.thi;
@@ -1483,39 +1143,17 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 }
                 return kTravDone;
             };
-#if RT_BVH4
             auto node_step = [&](int ref) -> int {
                 if (COUNT) cnt[CT_NODE] += 4;
                 return t4_step<STRIDE>(S, ref, f, thi, stk, sp);
             };
-#else
-            auto node_step = [&](int ref) -> int {
-                const RtTNode nd = S.tnodes[ref];
-                float ta, tb;
-                if (COUNT) cnt[CT_NODE] += 2;
-                const bool ha = slab(nd.box[0], f, thi, ta);
-                const bool hb = slab(nd.box[1], f, thi, tb);
-                if (ha && hb) {
-                    const bool a_first = ta <= tb;
-                    stk[sp * STRIDE] = (SK)(a_first ? nd.box[1].a : nd.box[0].a);
-                    ++sp;
-                    return a_first ? nd.box[0].a : nd.box[1].a;
-                }
-                if (ha || hb) return ha ? nd.box[0].a : nd.box[1].a;
-                return pop();
-            };
-#endif
-            // one round of closest_hit_fast's parked-leaf walk (RT_WALK_LEAVES = 2: a lane
-            // parks a second leaf and keeps stepping instead of idling until the leaf phase)
-            int ref = W.ref, leaf = W.leaf, leaf2 = kTravDone;
+            // one round of closest_hit_fast's parked-leaf walk
+            int ref = W.ref, leaf = W.leaf;
             while (ref >= 0) {
                 if (PROF) pcount<PROF>(*pf, PR_NODE);
                 ref = node_step(ref);
                 if (ref < 0 && ref != kTravDone && leaf == kTravDone) {
                     leaf = ref;
-                    ref = pop();
-                } else if (RT_WALK_LEAVES > 1 && ref < 0 && ref != kTravDone && leaf2 == kTravDone) {
-                    leaf2 = ref;
                     ref = pop();
                 }
                 if (__ballot(leaf == kTravDone) == 0ull) break;  // every walking lane holds a leaf
@@ -1529,10 +1167,7 @@ __device__ __forceinline__ void fast_walk_rounds(const DevScene& S, V3 o, V3 d, 
                 if (PROF) pcount<PROF>(*pf, PR_LEAF);
                 leaf_test<Real, COUNT, DEFER, L2>(S, leaf, r, f, thi, W.best_t, W.best, W.pk, W.plo, cnt);
                 leaf = kTravDone;
-                if (RT_WALK_LEAVES > 1 && leaf2 != kTravDone) {
-                    leaf = leaf2;
-                    leaf2 = kTravDone;
-                } else if (ref < 0 && ref != kTravDone) {
+                if (ref < 0 && ref != kTravDone) {
                     leaf = ref;
                     ref = pop();
                 }
@@ -1580,7 +1215,7 @@ __device__ __forceinline__ int closest_hit_brute(const DevScene& S, int n_prims,
     return best;
 }
 
-// Nearest-first brute force (RT_BRUTE_DEFER). The loop above runs primitive
+// Nearest-first brute force (up to kBruteMaxPrims primitives). The loop above runs primitive
 // k's exact test whenever ANY lane of the wave needs it - lanes hit different
 // walls, so a wave executes nearly every primitive's exact test per ray while
 // each lane needs about one. Here pass 1 (wave-uniform, scalar primitive
@@ -1589,9 +1224,6 @@ __device__ __forceinline__ int closest_hit_brute(const DevScene& S, int n_prims,
 // Pass 2 exact-tests each lane's candidates nearest-first through one
 // type-generic code path per primitive type, and stops once the nearest
 // remaining lower bound lies beyond the best hit. Same (t, slot) minimum.
-#ifndef RT_BRUTE_DEFER
-#define RT_BRUTE_DEFER 1
-#endif
 template <bool COUNT>
 __device__ __forceinline__ bool prim_maybe(const RtPrim& p, const FRay& f, float& lo, uint32_t* cnt) {
     const float thi = __builtin_inff();
@@ -1627,9 +1259,6 @@ __device__ __forceinline__ bool prim_exact(const RtPrim& p, const RayK<Real>& r,
 // costs the whole wave; the prologues stay per type, the division (the longest
 // piece of either) is shared. Same operations on the same operands: sphere_t's
 // (-h - sqrt(disc)) / a and aquad_t_rt's (D - n.o) / (n.d).
-#ifndef RT_NF_FUSED
-#define RT_NF_FUSED 1
-#endif
 template <class Real>
 __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Real>& r, Real& t) {
     const Real inf = (Real)__builtin_inf();
@@ -1709,10 +1338,7 @@ __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Rea
 // 1/2 + 1e-4, one FMA with source modifiers, compared against kWin (1e-6 more for that FMA's own
 // rounding); a NaN passes. Near-parallel rays (|d[a]| <= 1e-3 |d|, or a ray whose slab constants
 // overflowed: pthr = inf) are decided by the exact test.
-#ifndef RT_KET
-#define RT_KET 1e-6f  // (A/B: 1e-5f = the round-3 margin)
-#endif
-constexpr float kEt = RT_KET;
+constexpr float kEt = 1e-6f;
 constexpr float kWin = 0.5f + 1e-4f + 1e-6f;
 struct QuadPreRay {
     float c1, c0;
@@ -1828,8 +1454,7 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
             if (++n_exact == 2) cnt[CT_EXACT2]++;
         }
         Real t;
-        const bool hit = RT_NF_FUSED ? prim_exact_fused<Real>(S.prims[kb], ray_at_use<Real>(r), t)
-                                     : prim_exact<Real>(S.prims[kb], ray_at_use<Real>(r), t);
+        const bool hit = prim_exact_fused<Real>(S.prims[kb], ray_at_use<Real>(r), t);
         if (hit && (t < best_t || (t == best_t && kb < best))) {
             best_t = t;
             best = kb;
@@ -2078,13 +1703,13 @@ __device__ __forceinline__ const RtCamera& cam_opaque() {
 
 template <class Real, bool COUNT, int TRAV, class SK>
 __device__ __forceinline__ int closest_hit_any(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t, SK* stk,
-                                               float* stkt, uint32_t* cnt) {
+                                               uint32_t* cnt) {
     if (TRAV == TRAV_BRUTE) {
-        if (RT_BRUTE_DEFER && n_prims <= kBruteMaxPrims)
+        if (n_prims <= kBruteMaxPrims)
             return closest_hit_brute_nf<Real, COUNT>(S, n_prims, r, t, lot_column(stk), cnt);
         return closest_hit_brute<Real, COUNT>(S, n_prims, r, t, cnt);
     }
-    if (trav_fast(TRAV)) return closest_hit_fast<Real, COUNT, TRAV == TRAV_FAST_DEFER>(S, r, t, stk, stkt, cnt);
+    if (trav_fast(TRAV)) return closest_hit_fast<Real, COUNT, TRAV == TRAV_FAST_DEFER>(S, r, t, stk, cnt);
     return closest_hit<Real, COUNT>(S, r, t, stk, cnt);
 }
 
@@ -2170,11 +1795,7 @@ __device__ __forceinline__ V3 pixel_center(const RtCamera& C, int i, int j) {
 
 template <class Real, bool EMIT>
 __device__ __forceinline__ void path_begin(const RtCamera& C, Path<EMIT>& P, V3 pc, uint32_t pix, uint32_t sample) {
-#ifndef RT_ABL_NORNGINIT  // diagnostic ablation builds only
     P.rng = rng_init(C.seed_mix, pix, sample);
-#else
-    P.rng += (uint64_t)pix * 0x9E3779B97F4A7C15ull + sample;
-#endif
     const V3 du = ld3(C.du), dv = ld3(C.dv), cen = ld3(C.center);
     V3 ps = pc;
     if (C.samples > 1.0) {
@@ -2386,13 +2007,13 @@ __device__ __forceinline__ bool path_post(const DevScene& S, const RtCamera& C, 
 // path_post. Returns true when the path ends; `c` is then the sample's radiance
 // (the recursion's emitted + ... right fold included).
 template <class Real, bool EMIT, bool COUNT, bool PROF, int TRAV, class SK>
-__device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, Path<EMIT>& P, SK* stk, float* stkt,
-                                          uint32_t* cnt, unsigned long long& st_err, Prof& pf, V3& c) {
+__device__ __forceinline__ bool path_trip(const DevScene& S, const RtCamera& C, Path<EMIT>& P, SK* stk, uint32_t* cnt,
+                                          unsigned long long& st_err, Prof& pf, V3& c) {
     if (path_pre<Real, EMIT, PROF>(C, P, pf, c)) return true;
     const RayK<Real> ray = make_ray<Real>(P.o, P.d);
     Real t;
     if (COUNT) cnt[CT_RAYS]++;
-    const int h = closest_hit_any<Real, COUNT, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
+    const int h = closest_hit_any<Real, COUNT, TRAV>(S, C.n_prims, ray, t, stk, cnt);
     psec<PROF>(pf, PR_HIT);
     return path_post<Real, EMIT, COUNT, PROF>(S, C, P, h, t, cnt, st_err, pf, c);
 }
@@ -2504,8 +2125,7 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
     // the unused form folds away.
     S.nearfar = LDSS > 0 ? 1 : 0;
     if (LDSS > 0) {
-        S.qtree = 0;  // (compressed nodes and fp64 leaf records: trees walked from global memory only)
-        S.tsph2 = nullptr;
+        S.tsph2 = nullptr;  // (fp64 leaf records: trees walked from global memory only)
     }
     if (LDSS == 0) S.top_lds = reinterpret_cast<const char*>(lds_stack) + S0.lds_stack_bytes;
     if (LDSS > 0) {
@@ -2534,14 +2154,9 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
 // from the global copy.)
 template <int LDSS>
 __device__ __forceinline__ DevScene scene_prologue(const DevScene& S0, int* lds_stack) {
-    if (LDSS == 0 && S0.n_top > 0) {  // the tree's top: n_top nodes of 8 (compressed: 4) rows, a pad row each
+    if (LDSS == 0 && S0.n_top > 0) {  // the tree's top: n_top nodes of 8 rows, a pad row each
         uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_stack) + S0.lds_stack_bytes);
-        if (S0.qtree) {
-            const uint4* src = reinterpret_cast<const uint4*>(S0.qnodes);
-            for (int w = threadIdx.x; w < S0.n_top * 4; w += blockDim.x) dst[w + (w >> 2)] = src[w];
-        } else {
-            for (int w = threadIdx.x; w < S0.n_top * 8; w += blockDim.x) dst[w + (w >> 3)] = S0.blob[w];
-        }
+        for (int w = threadIdx.x; w < S0.n_top * 8; w += blockDim.x) dst[w + (w >> 3)] = S0.blob[w];
         __syncthreads();
     }
     if (LDSS > 0) {
@@ -2572,7 +2187,6 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
     StackT<LDSS>* stk = reinterpret_cast<StackT<LDSS>*>(lds_stack) + threadIdx.x;
-    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C.stack_depth * kStackStride + threadIdx.x;
 
     const int endX = min(reg.x + reg.width, C.width);
     const int endY = min(reg.y + reg.height, C.height);
@@ -2619,7 +2233,7 @@ __global__ __launch_bounds__(kBlock) void pt_render_kernel(DevScene S0, RtRegion
                 psec<PROF>(pf, PR_NEWPATH);
             }
             V3 c;
-            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(S, C, P, stk, stkt, cnt, st_err, pf, c)) {
+            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(S, C, P, stk, cnt, st_err, pf, c)) {
                 // PixelStats.add (renderStats.ts:76-88)
                 color = add(color, c);
                 ++n;
@@ -2706,9 +2320,6 @@ struct AdaptRound {
     int32_t horizon;        // sample count the round-length rule asks about (rt_api.cpp)
 };
 
-#ifndef RT_REC_NT
-#define RT_REC_NT 1
-#endif
 // One 16-byte sample record; NT: a non-temporal store. The pool kernel's records (read once,
 // by the accumulate pass) go out non-temporally: Cornell writes 4.27 GB per launch instead of
 // 4.78 GB for 2.62 GB of records (1.67x instead of 1.87x) at the same kernel time. The
@@ -2853,45 +2464,6 @@ __device__ __forceinline__ void item_decode(const SampleBuf& sb, const PhaseRow*
     s_end = s + r.chunk;
 }
 
-// Diagnostic (RT_WAVE_PROBE=1 variant builds only): per wave of a chunked / pool launch, the
-// real-time clock (100 MHz) at its start, when the hand-out ran dry for it and at its end, the
-// items it took and its hardware ids - where a launch's tail goes (tools/wave_probe.py).
-#ifndef RT_WAVE_PROBE
-#define RT_WAVE_PROBE 0
-#endif
-constexpr int kWaveProbeSlots = 8192;  // waves (256 CUs x 16 waves, twice over)
-#if RT_WAVE_PROBE
-static __device__ unsigned long long g_wave_probe[kWaveProbeSlots * 4];
-struct WaveProbe {
-    unsigned long long t0 = 0, tx = 0;
-    unsigned int items = 0;
-    __device__ void start() { t0 = __builtin_amdgcn_s_memrealtime(); }
-    __device__ void took(int n, bool exhausted) {
-        items += (unsigned int)n;
-        if (exhausted && tx == 0) tx = __builtin_amdgcn_s_memrealtime();
-    }
-    __device__ void finish(int lane, int waves_per_block) {
-        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        const int w = blockIdx.x * waves_per_block + (int)(threadIdx.x / kWave);
-        const unsigned int hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-        const unsigned int xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20); // XCC_ID
-        if (lane == 0 && w < kWaveProbeSlots) {
-            g_wave_probe[4 * w + 0] = t0;
-            g_wave_probe[4 * w + 1] = tx ? tx : t1;
-            g_wave_probe[4 * w + 2] = t1;
-            g_wave_probe[4 * w + 3] = ((unsigned long long)items << 32) | ((unsigned long long)(xcc & 0xf) << 28) |
-                                      (hw & 0x0fffffffu);
-        }
-    }
-};
-#else
-struct WaveProbe {
-    __device__ void start() {}
-    __device__ void took(int, bool) {}
-    __device__ void finish(int, int) {}
-};
-#endif
-
 // Item hand-out: every wave's first pool is static (wave w takes items
 // [w * pool, (w + 1) * pool)), the global counter deals the rest from
 // grid_waves * pool on - so the launch does not open with every wave's atomic
@@ -2918,14 +2490,8 @@ __device__ __forceinline__ void take_pool(const RenderOut& out, const SampleBuf&
     pool_end = min(base + sb.pool, sb.n_items);
 }
 
-#ifndef RT_DEFER_DIFFUSE
-#define RT_DEFER_DIFFUSE 0  // chunked kernel, resumable walks: diffuse shading batched to >= this many lanes
-#endif
-#ifndef RT_CHUNK_KOPQ
-#define RT_CHUNK_KOPQ 1  // 0: the A/B arm that keeps the launch parameters in SGPRs (profiles/r03/exp5_ckopq/)
-#endif
 // The chunked kernel's parameters as one block (the kernarg segment has this struct's layout).
-// With RT_CHUNK_KOPQ its trip loop reads them through an opaque kernarg pointer at each use
+// Its trip loop reads them through an opaque kernarg pointer at each use
 // (scalar loads from the constant cache) instead of keeping them live across the loop, where
 // the compiler ran out of SGPRs (106), spilled ~75 of them to VGPR lanes (v_writelane /
 // v_readlane, VALU issue) and spilled VGPRs to scratch: SGPR spills 72-75 -> 34-40 in the
@@ -2958,7 +2524,6 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
     StackT<LDSS>* stk = reinterpret_cast<StackT<LDSS>*>(lds_stack) + threadIdx.x;
-    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kStackStride + threadIdx.x;
     const int endX = min(reg.x + reg.width, C0.width);
     const int endY = min(reg.y + reg.height, C0.height);
     const int n_items = sb.n_items;
@@ -2973,8 +2538,6 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     Prof pf;
     prof_init<PROF>(pf, prof_lds, lane);
 
-    WaveProbe wprobe;
-    wprobe.start();
     int pool_next, pool_end;  // wave-uniform
     bool exhausted;           // wave-uniform
     first_pool(sb, pool_next, pool_end, exhausted);
@@ -2986,27 +2549,17 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
     Path<EMIT> P;
     const double rtx = 1.0 / (double)tiles_x;
     // resumable fast traversal (product builds): per-lane walk state across iterations
-    constexpr bool RS = RT_RESUME && trav_fast(TRAV) && INSTR != 1;  // (INSTR 2: timed sections)
+    // (round 5 also parked diffuse hits until 32 / 48 lanes waited, then shaded them together:
+    // 8-16 % slower - parked lanes are not walking; profiles/r05/defer_diffuse/)
+    constexpr bool RS = trav_fast(TRAV) && INSTR != 1;  // (INSTR 2: timed sections)
     FastWalk<Real> W;
     bool walking = false;
     LaneBounces lb;  // SampleBuf::rec12
-    // RT_DEFER_DIFFUSE (> 0, no emission stack): a path whose hit scatters diffusely waits for its
-    // light sampling until that many lanes of the wave do (pend_h: h | planar << 14 | front << 15,
-    // pend_mat: the Lambertian material; -1 = none)
-    constexpr int kDeferD = (RT_DEFER_DIFFUSE > 0 && !EMIT && RS) ? RT_DEFER_DIFFUSE : 0;
-    int pend_h = -1, pend_mat = 0;
 
-#if RT_CHUNK_KOPQ
 #define PK_SB (kern_args().sb)
 #define PK_REG (kern_args().reg)
 #define PK_OUT (kern_args().out)
 #define PK_S (scene_view<LDSS>(kern_args().S0, lds_stack))
-#else
-#define PK_SB sb
-#define PK_REG reg
-#define PK_OUT out
-#define PK_S S
-#endif
     while (true) {
         // hand out items to idle lanes (wave-uniform control flow); waits until
         // refill_min lanes are idle so the hand-out cost is shared
@@ -3014,7 +2567,6 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
         const int n_need = __popcll(need);
         if (n_need != 0 && !exhausted && (n_need >= PK_SB.refill_min || __ballot(slot >= 0) == 0ull)) {
             if (pool_next >= pool_end) take_pool(PK_OUT, PK_SB, lane, pool_next, pool_end, exhausted);
-            wprobe.took(exhausted ? 0 : min(n_need, pool_end - pool_next), exhausted);
             if (!exhausted) {
                 const int take = min(n_need, pool_end - pool_next);
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -3052,7 +2604,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             prof_trip<PROF>(pf);
             // lanes between rays: start a path if needed, then the level's depth
             // cut-off / roulette, and the walk of its ray
-            if (slot >= 0 && !walking && (!kDeferD || pend_h < 0)) {
+            if (slot >= 0 && !walking) {
                 if (new_path) {
                     path_begin<Real, EMIT>(C, P, pc, pix, (uint32_t)(PK_SB.s_base + s));
                     new_path = false;
@@ -3068,60 +2620,15 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
             psec<PROF>(pf, PR_RR);
             const bool was_walking = walking;
-            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF, kStackStride, LDSS == 0 && RT_TSPH2>(
+            fast_walk_rounds<Real, COUNT, TRAV == TRAV_FAST_DEFER, PROF, kStackStride, LDSS == 0>(
                 PK_S, P.o, P.d, W, walking, stk, PK_SB.min_ready, exhausted, cnt, &pf);
             psec<PROF>(pf, PR_HIT);
             // walks that ended: the rest of the level (miss / emission / scatter / light sampling)
             if (was_walking && !walking) {
                 fast_walk_resolve<Real, COUNT>(PK_S, P.o, P.d, W, cnt);
                 V3 c;
-                if constexpr (kDeferD) {
-                    // path_post up to the diffuse shading, which waits for its batch (below)
-                    const int h = W.best;
-                    if (h < 0) {
-                        finish_sample(miss_color<Real, EMIT, PROF>(C, P, st_err, pf));
-                    } else {
-                        V3 p, nrm, emitted, att, sdir;
-                        bool front, planar;
-                        int dmat = 0;
-                        const int kind = shade_hit<Real, EMIT, COUNT, PROF>(PK_S, P, h, W.best_t, cnt, pf, p, nrm, front,
-                                                                            planar, emitted, att, sdir, &dmat);
-                        if (kind == SC_NONE) {
-                            finish_sample(emitted);
-                        } else {
-                            ++P.bounces;
-                            P.o = p;
-                            if (kind == SC_SPEC) {
-                                P.T = mulv(P.T, att);
-                                P.d = sdir;
-                            } else {
-                                P.d = nrm;  // (as the pool kernel's D queue: the face normal rides in d)
-                                pend_h = h | (planar ? (1 << 14) : 0) | (front ? (1 << 15) : 0);
-                                pend_mat = dmat;
-                            }
-                        }
-                    }
-                } else {
-                    if (path_post<Real, EMIT, COUNT, PROF>(PK_S, C, P, W.best, W.best_t, cnt, st_err, pf, c))
-                        finish_sample(c);
-                }
-            }
-            if constexpr (kDeferD) {
-                // RT_DEFER_DIFFUSE: the mixture-PDF light sampling of the paths that wait for it, once
-                // kDeferD of them do (or no walk is left to overlap with): the same shade_diffuse call
-                // path_post makes, later - no draw of the path happens in between, so the draw order
-                // and the result are path_post's
-                const unsigned long long pm = __ballot(pend_h >= 0);
-                if (pm != 0ull && (__popcll(pm) >= kDeferD || exhausted || __ballot(walking) == 0ull)) {
-                    if (pend_h >= 0) {
-                        const int h = pend_h & 0x3fff;
-                        const V3 att = ld3(PK_S.mats[pend_mat].color);  // the Lambertian scatter's attenuation
-                        if (shade_diffuse<Real, EMIT, COUNT, PROF, 0>(PK_S, C, P, h, (pend_h >> 14) & 1,
-                                                                      (pend_h >> 15) & 1, P.o, P.d, att, cnt, pf))
-                            finish_sample(mulv(ld3(PK_S.mats[PK_S.prims[h].mat].emitted), P.T));
-                        pend_h = -1;
-                    }
-                }
+                if (path_post<Real, EMIT, COUNT, PROF>(PK_S, C, P, W.best, W.best_t, cnt, st_err, pf, c))
+                    finish_sample(c);
             }
             psec<PROF>(pf, PR_ACC);
         } else if (slot >= 0) {
@@ -3133,11 +2640,9 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
                 psec<PROF>(pf, PR_NEWPATH);
             }
             V3 c;
-            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(PK_S, C, P, stk, stkt, cnt, st_err, pf, c)) {
-#ifndef RT_ABL_NOSTORE  // diagnostic ablation builds only
+            if (path_trip<Real, EMIT, COUNT, PROF, TRAV>(PK_S, C, P, stk, cnt, st_err, pf, c)) {
                 rec_put<false>(PK_SB, (size_t)s * PK_SB.stride_s + (size_t)slot * PK_SB.stride_slot, c,
                                P.bounces | rec_err_bits(PK_SB.err_in_rec, st_err), lb, PK_OUT.stats);
-#endif
                 if (COUNT) {
                     cnt[CT_SAMPLES]++;
                     cnt[CT_BOUNCES] += (uint32_t)P.bounces;
@@ -3149,7 +2654,6 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
             }
         }
     }
-    wprobe.finish(lane, kBlockChunk / kWave);
     PixStats st;
     lb.to(st);
     publish_stats(out, st, st_err, lane);
@@ -3173,7 +2677,7 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 // otherwise. So the diffuse shading runs on full waves rather than on the
 // lanes whose path happens to need it in a given trip (the north star's
 // persistent-wavefront work queues). D is split by the mixture's branch
-// (RT_POOL_DSPLIT): A draws the mixture uniform ahead (on a copy of the path's
+// by branch: A draws the mixture uniform ahead (on a copy of the path's
 // RNG state; D draws the same value again) and queues the path for the
 // cosine-PDF or the light-PDF generate, so a D trip runs one of the two
 // sampling branches instead of both at half the lanes. Each path's arithmetic
@@ -3183,24 +2687,15 @@ __global__ __launch_bounds__(kBlockChunk) void pt_chunk_kernel(DevScene S0, RtRe
 #ifndef RT_POOL_K
 #define RT_POOL_K 152  // 56-byte slots + 2 queue bytes per wave, beside fp16 candidate columns
 #endif
-#ifndef RT_POOL_BLOCK
-#define RT_POOL_BLOCK 1024
-#endif
-#ifndef RT_POOL_DSPLIT
-#define RT_POOL_DSPLIT 1
-#endif
 #ifndef RT_POOL_PROF
 #define RT_POOL_PROF 0  // diagnostic variant: section timing (INSTR == 2 launches) in the pool kernel
 #endif
-#ifndef RT_POOL_ASPLIT
-#define RT_POOL_ASPLIT 1  // A queue split: paths to start (and slots needing an item) | paths in flight
-#endif
 constexpr int kPoolK = RT_POOL_K;          // path slots per wave
-constexpr int kBlockPool = RT_POOL_BLOCK;  // persistent workgroup size
+constexpr int kBlockPool = 1024;           // persistent workgroup size
 constexpr int kPoolGroups = 3;             // 16-byte groups per slot, plus one 8-byte group (below)
 static_assert(kPoolK >= kWave && kPoolK <= 256, "pool slots: one full wave, u8 queue entries");
 // Per wave: slot state as [group][slot] float4, then the A queue (a ring) and the D queue
-// (u8 slot indices; with RT_POOL_DSPLIT two stacks in one array: cosine-branch paths from
+// (u8 slot indices; two stacks in one array each. D: cosine-branch paths from
 // the bottom, light-branch paths from the top - together at most kPoolK entries).
 // 56 bytes per slot (more slots per wave fill more trips: 64 / 80 / 96 slots ran Cornell in
 // 21.7 / 17.7 / 16.1 ms, profiles/r02/poolsize/; 119 / 134 / 152 slots followed):
@@ -3230,18 +2725,6 @@ __device__ __forceinline__ int item_end(int s, int clog2) { return ((s >> clog2)
 constexpr size_t pool_lds_bytes() { return (size_t)(kBlockPool / kWave) * kPoolWaveBytes; }
 enum : int { PH_NEW = -1, PH_ITEM = -2 };  // next sample's path to start / no work item
 
-__device__ __forceinline__ int pool_ring(int x) { return x >= kPoolK ? x - kPoolK : x; }
-
-// Appends slot k of every lane with `want` to a queue (head, cnt wave-uniform).
-__device__ __forceinline__ void queue_push(uint8_t* q, int head, int& cnt, bool want, int k) {
-    const unsigned long long m = __ballot(want);
-    if (want) {
-        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        q[pool_ring(pool_ring(head + cnt) + r)] = (uint8_t)k;
-    }
-    cnt += __popcll(m);
-}
-
 // Stacks in one array: the bottom one fills [0, cnt), the top one [kPoolK - cnt, kPoolK).
 __device__ __forceinline__ void stack_push(uint8_t* q, bool top, int& cnt, bool want, int k) {
     const unsigned long long m = __ballot(want);
@@ -3262,7 +2745,6 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     const DevScene S = scene_prologue<LDSS>(S0, lds_stack);
     const int lane = threadIdx.x & (kWave - 1);
     StackT<LDSS>* stk = reinterpret_cast<StackT<LDSS>*>(lds_stack) + threadIdx.x;
-    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)C0.stack_depth * kStackStride + threadIdx.x;
     char* wpool = reinterpret_cast<char*>(lds_stack) + S0.lds_pool_off + (size_t)(threadIdx.x / kWave) * kPoolWaveBytes;
     float4* G = reinterpret_cast<float4*>(wpool);  // group q of slot k: G[q * kPoolK + k]
     float2* G3 = reinterpret_cast<float2*>(wpool + (size_t)kPoolK * kPoolGroups * 16);  // the 8-byte group
@@ -3283,15 +2765,13 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
         qa[k] = (uint8_t)k;
         G[k] = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f);
     }
-    int a_head = 0, a_cnt = kPoolK, d_head = 0, d_cnt = 0;  // wave-uniform queue state
-    int dl_cnt = 0;  // RT_POOL_DSPLIT: light-branch stack (d_cnt: cosine-branch stack)
-    // RT_POOL_ASPLIT: the A queue as two stacks in qa: paths to start from the bottom (an_cnt),
+    int a_cnt = kPoolK, d_cnt = 0;  // wave-uniform queue state
+    int dl_cnt = 0;  // the D queue's light-branch stack (d_cnt: cosine-branch stack)
+    // the A queue as two stacks in qa: paths to start from the bottom (an_cnt),
     // paths in flight from the top (ac_cnt); a_cnt stays their sum
     int an_cnt = kPoolK, ac_cnt = 0;
     int pool_next, pool_end;  // wave-uniform item hand-out
     bool exhausted;
-    WaveProbe wprobe;
-    wprobe.start();
     first_pool(sb, pool_next, pool_end, exhausted);
 
     // the sample's radiance and bounce count to its record; the slot's next phase
@@ -3300,7 +2780,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
     LaneBounces lb;  // SampleBuf::rec12
     auto record = [&](V3 c, int bounces, int slot, int& s, int s_end, unsigned long long err = 0ull) -> int {
         if (!sb.err_in_rec) st_err |= err;
-        rec_put<RT_REC_NT>(sb, (size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot, c,
+        rec_put<true>(sb, (size_t)s * sb.stride_s + (size_t)slot * sb.stride_slot, c,
                            bounces | (sb.err_in_rec ? (int)((uint32_t)err << kRecErrShift) : 0), lb, out.stats);
         ++s;
         return s < s_end ? PH_NEW : PH_ITEM;
@@ -3311,23 +2791,17 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
         __asm__ volatile("" ::: "memory");
         prof_trip<PP>(pf);
         psec<PP>(pf, PR_ACC);  // the previous trip's records, slot stores and queue appends
-        const bool dtop = RT_POOL_DSPLIT && dl_cnt > d_cnt;  // the longer D stack
+        const bool dtop = dl_cnt > d_cnt;  // the longer D stack
         const int dn = dtop ? dl_cnt : d_cnt;
-        const bool atop = RT_POOL_ASPLIT && ac_cnt > an_cnt;  // the longer A stack
-        const int an = RT_POOL_ASPLIT ? (atop ? ac_cnt : an_cnt) : a_cnt;
+        const bool atop = ac_cnt > an_cnt;  // the longer A stack
+        const int an = atop ? ac_cnt : an_cnt;
         if (dn >= kWave || dn > an) {
             // ---- D: diffuse shading of up to 64 queued paths ----
             const int n = min(kWave, dn);
             int k = -1, phase = 0;
-            if (RT_POOL_DSPLIT) {
-                if (lane < n) k = (int)qd[dtop ? kPoolK - dl_cnt + lane : d_cnt - n + lane];
-                if (dtop) dl_cnt -= n;
-                else d_cnt -= n;
-            } else {
-                if (lane < n) k = (int)qd[pool_ring(d_head + lane)];
-                d_head = pool_ring(d_head + n);
-                d_cnt -= n;
-            }
+            if (lane < n) k = (int)qd[dtop ? kPoolK - dl_cnt + lane : d_cnt - n + lane];
+            if (dtop) dl_cnt -= n;
+            else d_cnt -= n;
             if (k >= 0) {
                 const float4 g0 = G[k], g1 = G[kPoolK + k], g2 = G[2 * kPoolK + k];
                 const float2 g3 = G3[k];
@@ -3348,10 +2822,8 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 phase = P.bounces;
                 const RtCamera& C = cam_opaque();
                 const bool dterm =
-                    !RT_POOL_DSPLIT ? shade_diffuse<Real, false, false, PP, 0>(S, C, P, h, planar, front, P.o, P.d, att,
-                                                                               cnt, pf)
-                    : dtop ? shade_diffuse<Real, false, false, PP, 2>(S, C, P, h, planar, front, P.o, P.d, att, cnt, pf)
-                           : shade_diffuse<Real, false, false, PP, 1>(S, C, P, h, planar, front, P.o, P.d, att, cnt, pf);
+                    dtop ? shade_diffuse<Real, false, false, PP, 2>(S, C, P, h, planar, front, P.o, P.d, att, cnt, pf)
+                         : shade_diffuse<Real, false, false, PP, 1>(S, C, P, h, planar, front, P.o, P.d, att, cnt, pf);
                 if (dterm) {
                     // mixture value cut-off: the level's emission (as computed at the hit: T is unchanged)
                     const V3 c = mulv(ld3(S.mats[S.prims[h].mat].emitted), P.T);
@@ -3362,27 +2834,17 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 G[2 * kPoolK + k] = make_float4(P.d.x, P.d.y, P.d.z, P.T.x);
                 G3[k] = make_float2(P.T.y, P.T.z);
             }
-            if (RT_POOL_ASPLIT) {
-                stack_push(qa, false, an_cnt, k >= 0 && phase < 0, k);
-                stack_push(qa, true, ac_cnt, k >= 0 && phase >= 0, k);
-                a_cnt = an_cnt + ac_cnt;
-            } else {
-                queue_push(qa, a_head, a_cnt, k >= 0, k);
-            }
+            stack_push(qa, false, an_cnt, k >= 0 && phase < 0, k);
+            stack_push(qa, true, ac_cnt, k >= 0 && phase >= 0, k);
+            a_cnt = an_cnt + ac_cnt;
         } else {
             // ---- A: trace up to 64 queued paths ----
             const int n = min(kWave, an);
             int k = -1;
-            if (RT_POOL_ASPLIT) {
-                if (lane < n) k = (int)qa[atop ? kPoolK - ac_cnt + lane : an_cnt - n + lane];
-                if (atop) ac_cnt -= n;
-                else an_cnt -= n;
-                a_cnt -= n;
-            } else {
-                if (lane < n) k = (int)qa[pool_ring(a_head + lane)];
-                a_head = pool_ring(a_head + n);
-                a_cnt -= n;
-            }
+            if (lane < n) k = (int)qa[atop ? kPoolK - ac_cnt + lane : an_cnt - n + lane];
+            if (atop) ac_cnt -= n;
+            else an_cnt -= n;
+            a_cnt -= n;
             float4 g0 = make_float4(0.f, 0.f, pool_meta(PH_ITEM, 0, 0), 0.f), g1 = g0, g2 = g0;
             float2 g3 = make_float2(0.f, 0.f);
             if (k >= 0) {
@@ -3397,7 +2859,6 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
             const unsigned long long need = __ballot(k >= 0 && phase == PH_ITEM);
             if (need != 0ull && !exhausted) {
                 if (pool_next >= pool_end) take_pool(out, sb, lane, pool_next, pool_end, exhausted);
-                wprobe.took(exhausted ? 0 : min(__popcll(need), pool_end - pool_next), exhausted);
                 if (!exhausted) {
                     const int take = min(__popcll(need), pool_end - pool_next);
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -3443,11 +2904,11 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                     const RayK<Real> ray = make_ray<Real>(P.o, P.d);
                     Real t;
                     int h;
-                    if (PP && TRAV == TRAV_BRUTE && RT_BRUTE_DEFER && C.n_prims <= kBruteMaxPrims)  // section timer
+                    if (PP && TRAV == TRAV_BRUTE && C.n_prims <= kBruteMaxPrims)  // section timer
                         h = closest_hit_brute_nf<Real, false>(S, C.n_prims, ray, t, lot_column(stk), cnt,
                                                               [&]() { psec<PP>(pf, PR_TILE); });
                     else
-                        h = closest_hit_any<Real, false, TRAV>(S, C.n_prims, ray, t, stk, stkt, cnt);
+                        h = closest_hit_any<Real, false, TRAV>(S, C.n_prims, ray, t, stk, cnt);
                     psec<PP>(pf, PR_HIT);
                     if (h < 0) {
                         term = true;
@@ -3470,7 +2931,7 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                                 to_d = true;
                                 P.d = nrm;  // queued for D: g2 carries the face normal
                                 hf = h | (planar ? (1 << 14) : 0) | (front ? (1 << 15) : 0);
-                                if (RT_POOL_DSPLIT) {  // shade_diffuse's first draw and branch, ahead
+                                {  // shade_diffuse's first draw and branch, ahead
                                     uint64_t r = P.rng;
                                     const Real u0 = uniform<Real>(r);
                                     const Real rnd = S.mix_total == 1.0 ? u0 : u0 * (Real)S.mix_total;
@@ -3495,22 +2956,13 @@ __global__ __launch_bounds__(kBlockPool) void pt_pool_kernel(DevScene S0, RtRegi
                 G[2 * kPoolK + k] = g2;
                 G3[k] = g3;
             }
-            if (RT_POOL_ASPLIT) {
-                stack_push(qa, false, an_cnt, keep && !to_d && phase < 0, k);
-                stack_push(qa, true, ac_cnt, keep && !to_d && phase >= 0, k);
-                a_cnt = an_cnt + ac_cnt;
-            } else {
-                queue_push(qa, a_head, a_cnt, keep && !to_d, k);
-            }
-            if (RT_POOL_DSPLIT) {
-                stack_push(qd, false, d_cnt, to_d && !d_light, k);
-                stack_push(qd, true, dl_cnt, to_d && d_light, k);
-            } else {
-                queue_push(qd, d_head, d_cnt, to_d, k);
-            }
+            stack_push(qa, false, an_cnt, keep && !to_d && phase < 0, k);
+            stack_push(qa, true, ac_cnt, keep && !to_d && phase >= 0, k);
+            a_cnt = an_cnt + ac_cnt;
+            stack_push(qd, false, d_cnt, to_d && !d_light, k);
+            stack_push(qd, true, dl_cnt, to_d && d_light, k);
         }
     }
-    wprobe.finish(lane, kBlockPool / kWave);
     PixStats st;
     lb.to(st);
     publish_stats(out, st, st_err, lane);

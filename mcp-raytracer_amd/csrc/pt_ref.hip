@@ -13,19 +13,6 @@ hipError_t launch_render_ref(const KernelVariant& v, const DevScene& S, const Rt
     return dispatch_render<double>(v, S, reg, out, g, sb, stream);
 }
 
-#if RT_WAVE_PROBE
-// Diagnostic export of the wave probe (RT_WAVE_PROBE=1 variant builds only; pt_kernel.hpp
-// WaveProbe): reset = 1 zeroes it, else copies n words (4 per wave) to host memory.
-extern "C" int rt_debug_wave_probe(unsigned long long* host, int n, int reset) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_wave_probe)) != hipSuccess) return -1;
-    const size_t words = std::min<size_t>((size_t)std::max(n, 0), (size_t)kWaveProbeSlots * 4);
-    hipError_t e = reset ? hipMemset(p, 0, sizeof(g_wave_probe)) : hipMemcpy(host, p, words * 8, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    return e == hipSuccess ? 0 : -1;
-}
-#endif
-
 __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long* counters,
                                   unsigned int* tile_counter) {
     const int t = threadIdx.x;
@@ -35,9 +22,7 @@ __global__ void init_stats_kernel(unsigned long long* stats, unsigned long long*
 }
 
 constexpr int kAccBlock = 256;
-#ifndef RT_ACC_UNROLL
-#define RT_ACC_UNROLL 8
-#endif
+constexpr int kAccUnroll = 8;
 // Adds every pixel's samples in sample order (PixelStats.add), then
 // finalColor / u8 / RenderStats exactly as the sequential kernel.
 __global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegion reg, RenderOut out, int tiles_x,
@@ -54,7 +39,7 @@ __global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegi
             unsigned long long bsum = 0;
             int bmin = 0x7fffffff, bmax = 0;
             const int n = C.n_samples;
-            // RT_ACC_UNROLL loads in flight; sample-major records are coalesced across the
+            // kAccUnroll loads in flight; sample-major records are coalesced across the
             // wave, slot-major ones are one contiguous run per lane
             const size_t stride = (size_t)sb.stride_s;
             int k = 0;
@@ -63,12 +48,12 @@ __global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegi
                 // (addresses in floats: a 3-element vector type's size is 16 bytes, its loads 12)
                 const float* rec3 = reinterpret_cast<const float*>(sb.rec) + 3 * (size_t)slot * sb.stride_slot;
                 const size_t step = 3 * stride;
-                for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
-                    RecF3 r[RT_ACC_UNROLL];
+                for (; k + kAccUnroll <= n; k += kAccUnroll) {
+                    RecF3 r[kAccUnroll];
 #pragma unroll
-                    for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = *reinterpret_cast<const RecF3*>(rec3 + (size_t)(k + m) * step);
+                    for (int m = 0; m < kAccUnroll; ++m) r[m] = *reinterpret_cast<const RecF3*>(rec3 + (size_t)(k + m) * step);
 #pragma unroll
-                    for (int m = 0; m < RT_ACC_UNROLL; ++m) color = add(color, v3(r[m].x, r[m].y, r[m].z));
+                    for (int m = 0; m < kAccUnroll; ++m) color = add(color, v3(r[m].x, r[m].y, r[m].z));
                 }
                 for (; k < n; ++k) {
                     const RecF3 r = *reinterpret_cast<const RecF3*>(rec3 + (size_t)k * step);
@@ -76,12 +61,12 @@ __global__ __launch_bounds__(kAccBlock) void pt_accum_kernel(DevScene S0, RtRegi
                 }
             }
             const float4* rec = sb.rec + (size_t)slot * sb.stride_slot;
-            for (; k + RT_ACC_UNROLL <= n; k += RT_ACC_UNROLL) {
-                float4 r[RT_ACC_UNROLL];
+            for (; k + kAccUnroll <= n; k += kAccUnroll) {
+                float4 r[kAccUnroll];
 #pragma unroll
-                for (int m = 0; m < RT_ACC_UNROLL; ++m) r[m] = rec[(size_t)(k + m) * stride];
+                for (int m = 0; m < kAccUnroll; ++m) r[m] = rec[(size_t)(k + m) * stride];
 #pragma unroll
-                for (int m = 0; m < RT_ACC_UNROLL; ++m) {
+                for (int m = 0; m < kAccUnroll; ++m) {
                     color = add(color, v3(r[m].x, r[m].y, r[m].z));
                     const int b = __float_as_int(r[m].w);
                     bsum += (unsigned long long)b;
@@ -305,8 +290,7 @@ __global__ __launch_bounds__(kBlock) void world_hit_kernel(DevScene S, int n, co
     const RayK<double> r = make_ray<double>(o, d);
     double t = 0;
     int* stk = lds_stack + threadIdx.x;
-    float* stkt = reinterpret_cast<float*>(lds_stack) + (size_t)S.cam.stack_depth * kStackStride + threadIdx.x;
-    const int h = closest_hit_any<double, false, TRAV>(S, S.cam.n_prims, r, t, stk, stkt, nullptr);
+    const int h = closest_hit_any<double, false, TRAV>(S, S.cam.n_prims, r, t, stk, nullptr);
     double* w = out + 10 * (size_t)k;
     w[0] = h >= 0;
     w[1] = h >= 0 ? t : 0.0;

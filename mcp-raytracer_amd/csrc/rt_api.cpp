@@ -89,10 +89,6 @@ int device_cus(int dev) {
 // the smallest of: the units left, the record budget, and the counter headroom - a larger
 // record budget gives fewer, bounded passes instead of an error.
 constexpr long kItemCap = (1l << 31) - (1l << 22);
-#ifndef RT_QNODES_DEFAULT
-#define RT_QNODES_DEFAULT 0
-#endif
-constexpr bool kQnodesDefault = RT_QNODES_DEFAULT != 0;
 
 long pass_units(long units_left, long unit_slots, long chunks_per_slot, size_t rec_bytes_per_unit, size_t budget) {
     const long by_budget = (long)(budget / std::max<size_t>(rec_bytes_per_unit, 1));
@@ -172,7 +168,6 @@ struct DevCtx {
     int32_t lds_words = 0;    // [tnodes][tprims][tsph][prims] prefix, 16-byte words
     int32_t lds_words2 = 0;   // the same + [mats][lights]
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
-    int32_t off_q4 = -1;  // compressed 4-wide nodes (RtQ4Node) in the blob, or -1
     int32_t off_tsph2 = -1;  // leaf-order sphere records with the fp64 radius (RtLeafSph), or -1
     int32_t off_pre = 0;
     int32_t n_onb = 0;
@@ -326,8 +321,7 @@ struct DevCtx {
         if (dev != device) throw std::logic_error("device context used on another device");
         if (live) return;
         std::vector<char> blob;
-        if (RT_BVH4) append(blob, build.t4nodes, nullptr);  // the fast traversal's tree heads the blob
-        else append(blob, build.tnodes, nullptr);
+        append(blob, build.t4nodes, nullptr);  // the fast traversal's 4-wide tree heads the blob
         append(blob, build.tprims, &off_tprims);
         append(blob, build.tsph, &off_tsph);
         append(blob, build.prims, &off_prims);
@@ -339,8 +333,6 @@ struct DevCtx {
         lds_words2 = (int32_t)(blob.size() / 16);
         append(blob, build.nodes, &off_nodes);
         append(blob, prefilter_records(build.prims), &off_pre);
-        off_q4 = -1;
-        if (RT_BVH4 && !build.q4nodes.empty()) append(blob, build.q4nodes, &off_q4);
         off_tsph2 = -1;
         if (!build.tsph2.empty()) append(blob, build.tsph2, &off_tsph2);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
@@ -413,9 +405,7 @@ struct DevCtx {
         S.n_onb = n_onb;
         S.off_onbs = off_onbs;
         S.blob = d_blob;
-        S.qnodes = off_q4 >= 0 ? reinterpret_cast<const RtQ4Node*>(b + off_q4) : nullptr;
         S.tsph2 = nullptr;  // (set per launch: trees walked from global memory)
-        S.qtree = 0;
         S.lds_words = lds_words;
         S.off_prims = off_prims;
         S.off_mats = off_mats;
@@ -427,7 +417,7 @@ struct DevCtx {
         S.n_top = 0;         // set per launch when the tree is walked from global memory
         S.top_lds = nullptr;
         S.nearfar = 0;       // (scene_view sets it per LDS level)
-        S.troot = RT_BVH4 ? build.t4root : build.troot;
+        S.troot = build.t4root;
         S.root_box = build.troot_box;
         S.cam = build.cam;
         S.mix_total = host.mix_total;
@@ -465,7 +455,7 @@ struct DevCtx {
         const size_t lds_cap = (size_t)std::min(lds_max, kLdsSceneMaxBytes);
         // the LDS copy pads every 4-wide node to 144 bytes (pt_kernel.hpp t4_node: LDS bank windows)
         const int32_t node_pad =
-            RT_BVH4 && v.trav == TRAV_FAST && env_flag("RT_AMD_NODE_PAD", true) ? (int32_t)build.t4nodes.size() : 0;
+            v.trav == TRAV_FAST && env_flag("RT_AMD_NODE_PAD", true) ? (int32_t)build.t4nodes.size() : 0;
         g.lds_level = 0;
         if (lds_scene_enabled() && v.trav != TRAV_REFERENCE) {
             if (stack1 + (size_t)(lds_words2 + node_pad) * 16 <= lds_cap && env_flag("RT_AMD_LDS_MATS", true))
@@ -475,19 +465,17 @@ struct DevCtx {
         }
         // (16-bit stack entries hold node references < 2^15 and leaf codes ~(first << 3 | count) with
         // first < 2^12: always so for a tree that fits the LDS copy; checked)
-        if (g.lds_level > 0 && v.trav == TRAV_FAST && RT_STK16 &&
+        if (g.lds_level > 0 && v.trav == TRAV_FAST &&
             (build.t4nodes.size() >= (1u << 15) || build.tprims.size() >= (1u << 12)))
             g.lds_level = 0;
         const size_t stack = g.lds_level > 0 ? stack1 : stack0;
         g.lds_bytes = stack + (g.lds_level == 0 ? 0 : (size_t)((g.lds_level == 2 ? lds_words2 : lds_words) + node_pad) * 16);
         // a tree walked from global memory: its top (breadth-first prefix) in the LDS left beside the stack
         int32_t n_top = 0;
-        // a tree walked from global memory walks its compressed nodes (RtQ4Node: half the bytes per
-        // node, twice the nodes in the LDS top cache) where it has them; RT_AMD_QNODES=0/1 overrides
-        const bool qtree = g.lds_level == 0 && RT_BVH4 && v.trav == TRAV_FAST && off_q4 >= 0 &&
-                           env_flag("RT_AMD_QNODES", kQnodesDefault);
-        const size_t node_lds = qtree ? (size_t)kQ4LdsStride : sizeof(RtT4Node) + 16;
-        if (g.lds_level == 0 && RT_BVH4 && v.trav == TRAV_FAST && lds_scene_enabled() && env_flag("RT_AMD_TOP_CACHE", true)) {
+        // (round 5 also walked 8-bit quantised 64-byte nodes here, twice the nodes in the cache:
+        // 2 % slower, the decode costing more than the halved loads; profiles/r05/qnodes/)
+        const size_t node_lds = sizeof(RtT4Node) + 16;
+        if (g.lds_level == 0 && v.trav == TRAV_FAST && lds_scene_enabled() && env_flag("RT_AMD_TOP_CACHE", true)) {
             const size_t room = lds_cap > stack ? lds_cap - stack : 0;
             n_top = (int32_t)std::min<size_t>(build.t4nodes.size(), room / node_lds);
             g.lds_bytes = stack + (size_t)n_top * node_lds;
@@ -519,7 +507,6 @@ struct DevCtx {
         S.lds_words = g.lds_level == 2 ? lds_words2 : lds_words;
         S.lds_node_pad = g.lds_level > 0 ? node_pad : 0;
         S.n_top = n_top;
-        S.qtree = qtree ? 1 : 0;
         // trees walked from global memory: leaf records that carry the exact test's fp64 radius
         // (the LDSS-0 chunked kernels read them, pt_kernel.hpp leaf_test L2)
         S.tsph2 = off_tsph2 >= 0 ? reinterpret_cast<const RtLeafSph*>(reinterpret_cast<const char*>(d_blob) + off_tsph2)

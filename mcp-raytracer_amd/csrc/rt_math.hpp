@@ -52,13 +52,9 @@ template <class Real>
 RT_HD V3 scale(V3 a, Real t) {
     return V3{(float)((Real)a.x * t), (float)((Real)a.y * t), (float)((Real)a.z * t)};
 }
-#ifndef RT_FP64_SHORT
-// bit 0: unit vectors / Vec3.divide; bit 1: every Math.sqrt (pt_kernel.hpp m_sqrt). A/B at the
-// round-4 build (profiles/r04/fp64/): bit 0 alone is the fastest on the BVH scenes (spheres-500
-// path kernel 5.69 -> 5.62 ms, rain 41.9 -> 41.2 ms) and within 0.4 % on Cornell (13.84 -> 13.89
-// ms); bit 1 was no faster anywhere (its range test's branch costs what the scaling steps saved).
-#define RT_FP64_SHORT 1
-#endif
+// The correctly rounded restricted-domain forms below (rcp_rn / sqrt_rn) serve unit vectors and
+// Vec3.divide (A/B at the round-4 build, profiles/r04/fp64/: spheres-500 path kernel 5.69 -> 5.62
+// ms, rain 41.9 -> 41.2 ms, Cornell within 0.4 %).
 #if defined(__HIPCC__)
 // Correctly rounded double sqrt and reciprocal on a restricted domain, bit-identical there to the
 // compiler's general expansions (gfx950), which are the same instruction sequences plus range
@@ -107,7 +103,7 @@ __device__ __forceinline__ bool rcp_rn_ok(double y) {
 template <class Real>
 RT_HD Real recip(Real t) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (sizeof(Real) == 8 && (RT_FP64_SHORT & 1))
+    if constexpr (sizeof(Real) == 8)
         if (rcp_rn_ok(t)) return rcp_rn(t);
 #endif
     return (Real)1 / t;
@@ -117,7 +113,7 @@ RT_HD Real recip(Real t) {
 template <class Real>
 RT_HD Real rsqrt_rn(Real l) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (sizeof(Real) == 8 && (RT_FP64_SHORT & 1))
+    if constexpr (sizeof(Real) == 8)
         if (l < 0x1p300) return rcp_rn(sqrt_rn(l));
 #endif
     return (Real)1 / sqrt(l);

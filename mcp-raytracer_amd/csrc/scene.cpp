@@ -1015,57 +1015,6 @@ static std::vector<RtT4Node> t4_breadth_first(const std::vector<RtT4Node>& in) {
     return out;
 }
 
-bool make_q4nodes(const std::vector<RtT4Node>& t4, std::vector<RtQ4Node>& out) {
-    out.assign(t4.size(), RtQ4Node{});
-    for (size_t i = 0; i < t4.size(); ++i) {
-        const RtT4Node& n = t4[i];
-        RtQ4Node& q = out[i];
-        for (int k = 0; k < 4; ++k) q.ref[k] = n.ref[k];
-        for (int a = 0; a < 3; ++a) {
-            double lo = INFINITY, hi = -INFINITY;
-            for (int k = 0; k < 4; ++k) {
-                if (n.ref[k] == kT4Empty) continue;
-                const double l = n.bmin[a][k], h = n.bmax[a][k];
-                if (!std::isfinite(l) || !std::isfinite(h)) return false;  // planes: no quantised tree
-                lo = std::min(lo, l);
-                hi = std::max(hi, h);
-            }
-            if (!(lo <= hi)) lo = hi = 0.0;  // no child on this axis (all slots empty)
-            // the smallest power-of-two step whose 255-step grid from org = floor(lo / scl) * scl
-            // covers [lo, hi] with |org / scl| <= 2^23 (every grid point an exact fp32 fma)
-            int e = hi > lo ? (int)std::ceil(std::log2((hi - lo) / 255.0)) : -100;
-            e = std::max(e, -100);
-            double scl = 0.0, org = 0.0;
-            for (;; ++e) {
-                scl = std::ldexp(1.0, e);
-                const double N = std::floor(lo / scl);
-                org = N * scl;
-                if (std::fabs(N) <= 8388608.0 && std::ceil((hi - org) / scl) <= 255.0) break;
-            }
-            q.org[a] = (float)org;
-            q.scl[a] = (float)scl;
-            if ((double)q.org[a] != org || (double)q.scl[a] != scl) return false;
-            uint32_t wlo = 0, whi = 0;
-            for (int k = 0; k < 4; ++k) {
-                uint32_t bl = 255u, bh = 0u;  // empty slot: an inverted box (its reference decides anyway)
-                if (n.ref[k] != kT4Empty) {
-                    bl = (uint32_t)std::floor(((double)n.bmin[a][k] - org) / scl);
-                    bh = (uint32_t)std::ceil(((double)n.bmax[a][k] - org) / scl);
-                    // the decoded bounds (exact fp32 fma) contain the node's box
-                    if (!((double)std::fma((float)bl, q.scl[a], q.org[a]) <= (double)n.bmin[a][k]) ||
-                        !((double)std::fma((float)bh, q.scl[a], q.org[a]) >= (double)n.bmax[a][k]) || bh > 255u)
-                        throw std::runtime_error("quantised node does not contain its box");
-                }
-                wlo |= bl << (8 * k);
-                whi |= bh << (8 * k);
-            }
-            q.qlo[a] = wlo;
-            q.qhi[a] = whi;
-        }
-    }
-    return true;
-}
-
 std::vector<RtT4Node> make_t4nodes(const std::vector<RtNode>& f, int32_t& root_ref, int& depth) {
     std::vector<RtT4Node> out;
     depth = 0;
@@ -1421,7 +1370,6 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
             const std::vector<RtNode> padded = make_fast_nodes(sb.nodes);
             b.out.tnodes = make_tnodes(padded, b.out.troot);
             b.out.t4nodes = make_t4nodes(padded, b.out.t4root, b.out.t4depth);
-            if (!make_q4nodes(b.out.t4nodes, b.out.q4nodes)) b.out.q4nodes.clear();
             b.out.troot_box = padded[0];
             b.out.tdepth = sb.depth_seen;
         } else {
@@ -1455,7 +1403,7 @@ SceneBuild build_scene(const Value& scene_data, const Value* render_options) {
     // 4-wide tree (up to 3 pushes per level + 1). The 4-wide node step (pt_kernel.hpp t4_step)
     // writes up to sp + 2 whatever it pushes: at a node of level L the stack holds at most
     // 3 (L - 1) entries, so its writes stay below 3 t4depth entries - inside this bound.
-    cam.stack_depth = std::max(b.out.bvh_depth, RT_BVH4 ? 3 * b.out.t4depth + 1 : b.out.tdepth) + 1;
+    cam.stack_depth = std::max(b.out.bvh_depth, 3 * b.out.t4depth + 1) + 1;
     b.out.fast_ok = prims_inside_boxes(b.out.prims);
     return std::move(b.out);
 }

@@ -54,12 +54,7 @@ struct alignas(16) RtTNode {
 };
 static_assert(sizeof(RtTNode) == 64, "RtTNode must be 64 bytes");
 
-// Fast traversal over 4-wide nodes (1) or the binary children-in-parent tree (0).
-#ifndef RT_BVH4
-#define RT_BVH4 1
-#endif
-
-// 4-wide fast-traversal node (RT_BVH4): four children's boxes as [axis][child]
+// 4-wide fast-traversal node (the binary children-in-parent tree collapsed): four children's boxes as [axis][child]
 // rows (one ds_read_b128 per row) and their references (node index, leaf code
 // as in RtTNode, or kTravDone for an empty slot).
 struct alignas(16) RtT4Node {
@@ -70,25 +65,6 @@ struct alignas(16) RtT4Node {
 };
 static_assert(sizeof(RtT4Node) == 128, "RtT4Node must be 128 bytes");
 constexpr int32_t kT4Empty = (int32_t)0x80000000;  // empty child slot (= kTravDone)
-
-// Compressed 4-wide node (RT_AMD_QNODES; trees walked from global memory): the RtT4Node's
-// children's boxes quantised to 8 bits per plane against a per-node, per-axis grid
-// org[a] + q * scl[a] (scl a power of two, org a multiple of it with |org / scl| <= 2^23, so the
-// fp32 fma(q, scl, org) decodes every grid point exactly), rounded outward (lo down, hi up): each
-// decoded box contains the RtT4Node box, so the conservative slab test stays conservative.
-// 64 bytes = 4 rows: {org.xyz, scl.x}, {scl.yz, qlo.x, qlo.y}, {qlo.z, qhi.xyz}, {ref[4]};
-// qlo / qhi[a] hold child c's byte at bits 8c .. 8c + 7.
-struct alignas(16) RtQ4Node {
-    float org[3];
-    float scl[3];
-    uint32_t qlo[3];
-    uint32_t qhi[3];
-    int32_t ref[4];
-};
-static_assert(sizeof(RtQ4Node) == 64, "RtQ4Node must be 64 bytes");
-// The quantised copy of a 4-wide tree (same numbering, same references); false when a node has
-// an infinite bound (planes) - the tree then keeps its 128-byte nodes only.
-bool make_q4nodes(const std::vector<struct RtT4Node>& t4, std::vector<RtQ4Node>& out);
 
 // Leaf-order sphere record for trees walked from global memory (tsph2, per tprims entry): the
 // fp32 pre-filter's {centre, fp32 radius}, the exact test's fp64 radius (the JS double) and the
@@ -204,8 +180,7 @@ struct SceneBuild {
     std::vector<int32_t> tprims; // its leaves' primitive slots (padded to a multiple of 4)
     std::vector<float> tsph;     // per tprims entry: sphere {centre, fp32 radius}, NaNs for other types
     std::vector<RtLeafSph> tsph2; // per tprims entry: the same + fp64 radius + slot (trees walked from global memory)
-    std::vector<RtT4Node> t4nodes; // the same tree collapsed to 4-wide nodes (RT_BVH4)
-    std::vector<RtQ4Node> q4nodes; // ... quantised (empty when some bound is infinite)
+    std::vector<RtT4Node> t4nodes; // the same tree collapsed to 4-wide nodes (the device walks these)
     int32_t t4root = 0;          // its root reference
     int t4depth = 0;             // its depth in 4-wide nodes
     int32_t troot = 0;           // reference of the root (TNode index or leaf code)

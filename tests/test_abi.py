@@ -40,10 +40,11 @@ def test_product_kernels_do_not_spill_to_scratch(rt):
     import sys
     from pathlib import Path
     from raytracer_amd import _lib
+    pytest.importorskip("msgpack", reason="the AMDGPU metadata note is msgpack (tools/kernel_resources.py)")
     sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
     import kernel_resources
     ks = kernel_resources.resources(_lib.LIB_PATH)
-    assert len(ks) > 40
+    assert len(ks) > 40, f"only {len(ks)} kernels found in the gfx950 code objects"
     # pt_pool_kernel<Real, TRAV, LDSS>; pt_chunk_kernel / pt_render_kernel<Real, EMIT=false, INSTR=0, ...>
     product = re.compile(r"pt_pool_kernel|pt_(chunk|render)_kernelI[df]Lb0ELi0E|pt_accum_kernel|pt_adapt_kernel")
     checked = [k for k in ks if product.search(k["name"])]
@@ -268,15 +269,3 @@ def test_pass_plan_caps_items_at_the_counter_headroom(rt):
     assert plan(10, 64, 16, 1 << 20, 1) == 1
     with pytest.raises(_lib.RtError):
         plan(10, 0, 16, 1000, 1 << 30)
-
-
-def test_compressed_nodes_build_for_sphere_trees(rt):
-    """make_q4nodes (scene.cpp) quantises every 4-wide node's child boxes to 8-bit grids and
-    asserts on the host that each decoded box (an exact fp32 fma) contains the node's box -
-    camera creation throws otherwise. Sphere fields of several sizes and seeds, incl. one
-    whose tree is walked from global memory (the compressed nodes' use)."""
-    for count, seed in ((50, 1), (500, 42), (6000, 9), (20000, 5)):
-        sd = rt.generate_scene_data({"type": "spheres", "options": {"count": count, "seed": seed}})
-        cam = rt.create_camera_from_scene_data(sd, {"width": 16, "samples": 1, "aTolerance": 0})
-        assert cam.info["n_objects"] >= 1
-        cam.close()

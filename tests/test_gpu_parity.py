@@ -352,9 +352,17 @@ def test_adaptive_rounds_ignore_misses_past_convergence(rt, oracle, gpu, path, m
     cam, rgb, rad, st = _render_gpu(rt, sd, ro, region=region)
     assert cam.last_kernel() == ("chunked" if path != "pool" else "pool")
     rounds, rendered = cam.adaptive_info()
-    # the round in which the pixel converges ([40, 130), or [10, 200) when the round-length rule
-    # takes the rest after round 1) rendered sample 71 - a miss - past the convergence at 60
-    assert rounds in (2, 3) and rendered >= 72
+    # round 1 retires none of the region's one pixel, so the round-length rule takes the rest:
+    # [0, 10), [10, 200) - the round in which the pixel converges rendered sample 71 (a miss)
+    assert rounds == 2 and rendered == 200
+    # without the rule (RT_AMD_ADAPT_JUMP=0: rounds grow x3) [0, 10), [10, 40), [40, 130): the
+    # third round renders sample 71 past the convergence at 60
+    monkeypatch.setenv("RT_AMD_ADAPT_JUMP", "0")
+    cam3, rgb3, rad3, st3 = _render_gpu(rt, sd, ro, region=region)
+    assert cam3.adaptive_info() == (3, 130)
+    assert_identical(rad3[:1, :1], rgb3[:1, :1], orc["radiance"][:1, :1], orc["rgb"][:1, :1], f"slit box {path} x3")
+    assert_stats_identical(st3, orc["stats"])
+    monkeypatch.delenv("RT_AMD_ADAPT_JUMP")
     assert_identical(rad[:1, :1], rgb[:1, :1], orc["radiance"][:1, :1], orc["rgb"][:1, :1], f"slit box {path}")
     assert_stats_identical(st, orc["stats"])
     # fixed spp renders sample 71 for real: the reference's error
@@ -430,6 +438,34 @@ def test_axis_quad_edges_and_corners(rt, oracle, gpu):
     d = (targets - o).astype(np.float32)
     c = _hit_equal(rt, oracle, sd, o.astype(np.float32), d)
     assert (c[:, 0] > 0).mean() > 0.5
+
+
+@pytest.mark.parametrize("cfg", [{"type": "cornell"}, {"type": "spheres", "options": {"count": 500, "seed": 42}},
+                                 {"type": "spheres", "options": {"count": 6000, "seed": 9}}],
+                         ids=["cornell", "spheres500", "spheres6000"])
+def test_near_parallel_rays_match_oracle(rt, oracle, gpu, cfg):
+    """make_fray leaves an axis with 0 < |d_a| < 1e-3 max|d| out of the slab test's
+    absolute slack (pt_kernel.hpp make_fray): rays whose components are +-1e-4, 1e-6 and 1e-9
+    times max|d| on one or two axes, from origins at |o| = 10 .. 1e4 aimed at the scene, through
+    the fast walk (and brute force) against the reference-order traversal and the oracle."""
+    sd = rt.generate_scene_data(cfg)
+    rng = np.random.default_rng(17)
+    n = 3000
+    centre = np.float64([278, 278, 278]) if cfg["type"] == "cornell" else np.float64([0, 1, 0])
+    rad = 10.0 ** rng.uniform(1, 4, n)
+    dirn = rng.normal(size=(n, 3))
+    dirn /= np.linalg.norm(dirn, axis=1, keepdims=True)
+    o = centre + rad[:, None] * dirn
+    d = centre + rng.normal(scale=2.0, size=(n, 3)) - o
+    scale = np.float64([1e-4, 1e-6, 1e-9])[rng.integers(0, 3, n)] * np.abs(d).max(axis=1)
+    sign = np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    ax = rng.integers(0, 3, n)
+    d[np.arange(n), ax] = sign * scale
+    two = rng.random(n) < 0.3  # a second near-parallel axis
+    ax2 = (ax + 1 + rng.integers(0, 2, n)) % 3
+    d[np.arange(n)[two], ax2[two]] = -sign[two] * scale[two]
+    travs = ("reference", "fast", "brute") if cfg["type"] == "cornell" else ("reference", "fast")
+    _hit_equal(rt, oracle, sd, o.astype(np.float32), d.astype(np.float32), travs=travs)
 
 
 def test_sah_tree_on_surface_and_grazing_rays(rt, oracle, gpu):
@@ -588,14 +624,14 @@ def test_large_scene_global_traversal(rt, oracle, gpu, monkeypatch):
     sd = rt.generate_scene_data({"type": "spheres", "options": {"count": 6000, "seed": 9}})
     ro = {"width": 96, "aspect": 1, "samples": 8, "depth": 12, **NOADAPT}
     outs = []
-    # (the fast walks both on the 128-byte 4-wide nodes and on the compressed 64-byte ones)
     # (the chunked kernels read the fp64 leaf records, tsph2; the sequential kernel of the
-    # reference-order pass does not), and with SAH leaves of 1 (this size's default), 2 and 4
-    for trav, defer, q, leaf in (("reference", "0", "0", "1"), ("fast", "0", "0", "1"), ("fast", "1", "0", "1"),
-                                 ("fast", "0", "1", "1"), ("fast", "1", "1", "1"), ("fast", "0", "0", "2"),
-                                 ("fast", "0", "0", "4")):
+    # reference-order pass does not), with and without deferred exact tests and the LDS top
+    # cache, and with SAH leaves of 1 (this size's default), 2 and 4
+    for trav, defer, top, leaf in (("reference", "0", "1", "1"), ("fast", "0", "1", "1"), ("fast", "1", "1", "1"),
+                                   ("fast", "0", "0", "1"), ("fast", "1", "0", "1"), ("fast", "0", "1", "2"),
+                                   ("fast", "0", "1", "4")):
         monkeypatch.setenv("RT_AMD_DEFER", defer)
-        monkeypatch.setenv("RT_AMD_QNODES", q)
+        monkeypatch.setenv("RT_AMD_TOP_CACHE", top)
         monkeypatch.setenv("RT_AMD_SAH_MAXLEAF", leaf)
         cam, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": trav})
         outs.append((rgb, rad, st))
@@ -1074,6 +1110,9 @@ def test_adaptive_full_size_headline_rows_match_oracle(rt, oracle, gpu):
     ro = {"width": 800, "samples": 256, "depth": 16}
     cam, rgb, rad, st = _render_gpu(rt, sd, ro)
     assert cam.last_kernel() == "pool"
+    # round 1 (10 samples) retires 17 % of the pixels, and few carried pixels are likely to
+    # converge within a grown round: the round-length rule takes the rest (2 rounds)
+    assert cam.adaptive_info()[0] == 2
     W, H = cam.image_width, cam.image_height
     assert st.pixels == W * H and st.samples["min"] < 256 and st.samples["max"] == 256
     for y in (0, 311, 400, 799):
@@ -1088,6 +1127,16 @@ def test_adaptive_full_size_headline_rows_match_oracle(rt, oracle, gpu):
         del os.environ["RT_AMD_ADAPT_ROUNDS"]
     assert_identical(rad, rgb, rad2, rgb2, "adaptive 800 rounds == sequential")
     assert st.samples == st2.samples and st.bounces == st2.bounces
+    # the likely-to-converge arm off (RT_AMD_ADAPT_LIKELY=0): round 1's 17 % keeps the rounds
+    # growing x3 - [0, 10), [10, 40), [40, 256) - and the image is the same
+    os.environ["RT_AMD_ADAPT_LIKELY"] = "0"
+    try:
+        cam3, rgb3, rad3, st3 = _render_gpu(rt, sd, ro)
+    finally:
+        del os.environ["RT_AMD_ADAPT_LIKELY"]
+    assert cam3.adaptive_info()[0] == 3
+    assert_identical(rad, rgb, rad3, rgb3, "adaptive 800 likely rule off")
+    assert st.samples == st3.samples and st.bounces == st3.bounces
 
 
 # ---------------------------------------------------------------------------

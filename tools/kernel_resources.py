@@ -38,11 +38,18 @@ def _sections(elf: bytes) -> dict:
     return out
 
 
+CCOB_MAGIC = b"CCOB"  # clang's compressed offload bundle (not parsed here)
+
+
 def code_objects(lib: Path, target: str = "gfx950"):
     """Yield the device code objects for `target` in the library's offload bundles."""
     data = lib.read_bytes()
     off, size = _sections(data)[".hip_fatbin"]
     fat = data[off:off + size]
+    if BUNDLE_MAGIC not in fat:
+        kind = "compressed (CCOB) bundles" if CCOB_MAGIC in fat else "no offload bundle"
+        raise RuntimeError(f"{lib.name}: .hip_fatbin holds {kind}; this reader parses uncompressed "
+                           f"{BUNDLE_MAGIC.decode()} bundles only (build without --offload-compress)")
     for m in re.finditer(re.escape(BUNDLE_MAGIC), fat):
         base = m.start()
         n, = struct.unpack_from("<Q", fat, base + len(BUNDLE_MAGIC))

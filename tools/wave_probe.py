@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Where a launch's tail goes: per-wave start / hand-out-dry / end times of one render.
 
-Needs the diagnostic variant library built with RT_WAVE_PROBE=1 (run with
+Needs the diagnostic variant library built from a tree with tools/wave_probe.patch applied
+(the probe is not in the product kernel) and RT_WAVE_PROBE=1 (run with
 RT_AMD_VARIANT=<its name>): every wave of a chunked / pool launch records the 100 MHz real-time
 clock at its start, when the item hand-out ran dry for it, and at its end, plus its item count
 and hardware ids (pt_kernel.hpp WaveProbe). For each scene and tile-group count N it renders
