@@ -341,13 +341,33 @@ def main(argv=None):
         cam_c.close()
         log(f"work counters: {int(st_c.samples['total'])} samples counted")
 
+    # Rank 0's frame goes to pinned host memory on a copy stream, double-buffered: frame k's D2H
+    # copy overlaps frame k+1's render (which writes the other device frame), and frame k+2 waits
+    # for frame k's copy before it reuses its buffer. Every timed frame still reaches the host
+    # inside the timed region (the closing synchronize waits for the copy stream too).
+    frames = [frame, torch.zeros_like(frame)] if rank == 0 else [frame, frame]
+    host_frames = [host_frame, torch.zeros_like(host_frame, pin_memory=True)] if rank == 0 else None
+    copy_stream = torch.cuda.Stream(dev) if rank == 0 else None
+    rendered = [torch.cuda.Event(), torch.cuda.Event()]
+    copied = [torch.cuda.Event(), torch.cuda.Event()]  # (waiting on a never-recorded event is a no-op)
+    nstep = [0]
+
     def step():
-        if world == 1:
-            cam.render_device(rgb_ptr=frame.data_ptr(), stream=sptr)
-        else:
-            rtd.render_frame(cam, frame, rank, world, stream=sptr, slab=slab, gathered=gathered)
+        b = nstep[0] % 2
+        nstep[0] += 1
         if rank == 0:
-            host_frame.copy_(frame, non_blocking=True)  # D2H on the same stream, inside the timed step
+            stream.wait_event(copied[b])  # frame k-2's copy has read this buffer
+        fr = frames[b]
+        if world == 1:
+            cam.render_device(rgb_ptr=fr.data_ptr(), stream=sptr)
+        else:
+            rtd.render_frame(cam, fr, rank, world, stream=sptr, slab=slab, gathered=gathered)
+        if rank == 0:
+            rendered[b].record(stream)
+            copy_stream.wait_event(rendered[b])
+            with torch.cuda.stream(copy_stream):
+                host_frames[b].copy_(fr, non_blocking=True)  # D2H inside the timed step
+            copied[b].record(copy_stream)
 
     # this rank's share (untimed): pixels and samples per launch
     st, _ = cam.render_device(rgb_ptr=frame.data_ptr(), tile_group=rank, tile_groups=world, stream=sptr,
@@ -401,7 +421,7 @@ def main(argv=None):
     # Untimed: the same frame again with its fp32 radiance (assembled over the ranks
     # like the timed frames) and the merged RenderStats, for the checks below.
     radiance = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
-    timed_rgb = host_frame.numpy().copy() if rank == 0 else None
+    timed_rgb = host_frames[(nstep[0] - 1) % 2].numpy().copy() if rank == 0 else None
     res = rtd.render_frame(cam, frame, rank, world, stream=sptr, radiance=radiance, stats=True)
     torch.cuda.synchronize()
     frame_check = None
@@ -457,7 +477,8 @@ def main(argv=None):
                                       (" + RCCL gather of tile-packed slabs to rank 0" if world > 1 else "")},
             "build_id": rt.build_id(),
             **({"frame_check": frame_check} if args.check else {}),
-            "host_copy": "each timed step ends with rank 0's u8 frame copied into pinned host memory",
+            "host_copy": "each timed step copies rank 0's u8 frame into pinned host memory (copy stream, "
+                         "double-buffered: frame k's copy overlaps frame k+1's render; all inside the timed region)",
             "parity": parity,
             "roofline": rl,
             "cpu_baseline": cpu,

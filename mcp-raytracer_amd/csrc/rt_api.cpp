@@ -742,7 +742,8 @@ struct DevCtx {
         for (int s_base = 0; n_act > 0 && s_base < C.n_samples; s_base += len, len = take_rest ? C.n_samples : len * grow) {
             len = std::min(len, C.n_samples - s_base);
             ++adapt_rounds;
-            adapt_rendered += (unsigned long long)n_act * (unsigned long long)len;
+            // round 0 numbers every slot of the launch's tiles; only the pixels inside the region render
+            adapt_rendered += (unsigned long long)(act ? n_act : region_pixels(reg, mine)) * (unsigned long long)len;
             if (trace) std::fprintf(stderr, "[rt adaptive] round %d: samples [%d, %d) of %ld pixels\n", adapt_rounds,
                                     s_base, s_base + len, n_act);
             ar.len = len;
@@ -782,6 +783,19 @@ struct DevCtx {
                         ((double)(n_prev - n_act) < (double)jump * 1e-3 * (double)n_prev ||
                          (likely_pm > 0 && (double)n_likely < (double)likely_pm * 1e-3 * (double)n_act));
         }
+    }
+
+    // Pixels inside the region among the `mine` tiles this launch owns (tile t of the region is
+    // owned iff t % tile_groups == tile_group, as the kernels' item_pixel maps them).
+    static long region_pixels(const RtRegion& reg, long mine) {
+        const int tiles_x = std::max((reg.width + kTile - 1) / kTile, 1);
+        long n = 0;
+        for (long k = 0; k < mine; ++k) {
+            const long t = reg.tile_group + k * reg.tile_groups;
+            const int tx = (int)(t % tiles_x), ty = (int)(t / tiles_x);
+            n += (long)std::min(kTile, reg.width - tx * kTile) * std::min(kTile, reg.height - ty * kTile);
+        }
+        return n;
     }
 
     int adapt_rounds = 0;                   // rounds of the last adaptive render

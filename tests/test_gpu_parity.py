@@ -359,7 +359,7 @@ def test_adaptive_rounds_ignore_misses_past_convergence(rt, oracle, gpu, path, m
     # third round renders sample 71 past the convergence at 60
     monkeypatch.setenv("RT_AMD_ADAPT_JUMP", "0")
     cam3, rgb3, rad3, st3 = _render_gpu(rt, sd, ro, region=region)
-    assert cam3.adaptive_info() == (3, 130)
+    assert cam3.adaptive_info() == (3, 130)  # 10 + 30 + 90 samples of the one pixel
     assert_identical(rad3[:1, :1], rgb3[:1, :1], orc["radiance"][:1, :1], orc["rgb"][:1, :1], f"slit box {path} x3")
     assert_stats_identical(st3, orc["stats"])
     monkeypatch.delenv("RT_AMD_ADAPT_JUMP")

@@ -12,7 +12,6 @@
 #   prof              bench under rocprofv3 --kernel-trace --stats (csv)
 #   valu / traffic    the VALU / HBM counter passes of the bench configs + fp32 + adaptive (separate --pmc runs)
 #   valu5 / traffic5  the same for BASELINE config 5 (spheres-100k 4096^2 spp1024 depth 100, 32 passes)
-#   pcsample          rocprofv3 stochastic PC sampling of two headline frames (tools/render_frames.py)
 #   rankshare         tools/rank_share.py: every tile group of N = 2, 4, 8 (max / min / mean) + RCCL gather + unpack
 #   sections          tools/profile_sections.py (section timers of the chunked / sequential kernels)
 #   poolsections      the same for the pool kernel (variant library 'poolprof': RT_POOL_PROF=1, RT_POOL_K=146)
@@ -63,11 +62,6 @@ for step in "$@"; do
     valu5) VALU_DIR=$O/valu5 bash tools/pmc_valu.sh "$CFG5" || exit $? ;;
     traffic) TRAFFIC_DIR=$O/traffic bash tools/pmc_traffic.sh "${CFGS4[@]}" "--precision fp32" "--adaptive" || exit $? ;;
     traffic5) TRAFFIC_DIR=$O/traffic5 bash tools/pmc_traffic.sh "$CFG5" || exit $? ;;
-    pcsample)  # stochastic PC sampling (rocprofv3 beta) of the headline frames: instruction hot spots
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled \
-        --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 65536 \
-        -d $R/$O/pcs -o run --output-format csv -- python3 $R/tools/render_frames.py --frames 2 \
-        > $R/$O/pcsample.log 2>&1) || exit $? ;;
     rankshare) run 400 rank_share.log python tools/rank_share.py cornell spheres rain || exit $? ;;
     sections) run 300 sections.log python tools/profile_sections.py || exit $? ;;
     sections:*) run 300 sections_${step#sections:}.log python tools/profile_sections.py ${step#sections:} || exit $? ;;
