@@ -448,6 +448,16 @@ def main(argv=None):
         rl = roofline(key, rt.build_id(), my_samples, kernel_ms, counters, my_pixels)
         rl.update({"kernel": kernel_name, "accum_kernel_ms": round(accum_ms, 4), "passes": passes,
                    "count_subsample": sub})
+        if accum_ms > 0 and not args.adaptive:
+            # the in-order accumulate pass (pt_accum_kernel) is the HBM-bound kernel of the frame: it
+            # streams every sample's record (12 B {r, g, b} at fixed spp in colour mode, 16 B with
+            # the bounce word) once and writes each pixel's u8 RGB (3 B); algorithmic bytes / its time
+            rec_b = 16 if cam.info["mode"] == 1 else 12  # MODE_BOUNCES keeps the bounce word
+            ab = my_samples * rec_b + my_pixels * 3
+            gbs = ab / (accum_ms / 1e3) / 1e9
+            rl["accumulate"] = {"kernel": "pt_accum_kernel", "bound": "hbm", "achieved": round(gbs, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                "algorithmic_bytes_per_launch": ab, "record_bytes_per_sample": rec_b}
         if args.adaptive:
             rl["adaptive_rounds"] = {"rounds": a_rounds, "samples_rendered": a_rendered,
                                      "samples_kept": int(my_samples),
