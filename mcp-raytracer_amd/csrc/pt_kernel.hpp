@@ -41,6 +41,7 @@ struct DevScene {
     const RtPrim* __restrict__ prims;   // global, or LDS in an LDS-resident launch
     const RtPrim* __restrict__ gprims;  // always the global copy (scalar-load reads)
     const RtPre* __restrict__ gpre;     // brute-force pre-filter records (global, scalar-load reads)
+    int32_t n_pre;                      // ... and their count (pairs count once)
     const int32_t* __restrict__ tprims; // fast-traversal leaves -> primitive slots (LDS when resident)
     const float4* __restrict__ tsph;    // per tprims entry: sphere {centre, fp32 radius} or NaNs (LDS when resident)
     const RtMat* __restrict__ mats;
@@ -1368,14 +1369,77 @@ __device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, c
     return !(wa > kWin) && !(wb > kWin);
 }
 
+// Pre-filters of a PAIR of primitives in packed fp32 (RtPre PRE_SPHERE2 / PRE_QUAD2): the same
+// operations as sphere_maybe / aquad_maybe_pre, element by element, on two-float vectors that
+// the compiler issues as v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (one instruction for both
+// primitives; the record's element pairs sit in aligned SGPR pairs, the ray's operands are
+// broadcast with op_sel). Branch-free: both results are computed and masked. The margins are
+// the single tests' (a filter may round differently as long as it stays conservative; the
+// pair's window margin uses the larger qk of the two).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pf2_of(float x) { return pf2{x, x}; }
+__device__ __forceinline__ pf2 pf2_fma(pf2 a, pf2 b, pf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ pf2 pf2_abs(pf2 a) { return __builtin_elementwise_abs(a); }
+
+__device__ __forceinline__ void sphere_maybe2(const float* v, const FRay& f, bool& m0, bool& m1, float& lo0,
+                                              float& lo1) {
+    RT_FP32_FUSED
+    const pf2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, r = {v[6], v[7]}, rr = {v[8], v[9]};
+    const pf2 ox = pf2_of(f.o[0]) - cx, oy = pf2_of(f.o[1]) - cy, oz = pf2_of(f.o[2]) - cz;
+    const pf2 b = pf2_fma(oz, pf2_of(f.d[2]), pf2_fma(oy, pf2_of(f.d[1]), ox * pf2_of(f.d[0])));
+    const pf2 oo = pf2_fma(oz, oz, pf2_fma(oy, oy, ox * ox));
+    const pf2 disc = pf2_fma(b, b, -(pf2_of(f.a) * (oo - rr)));
+    const pf2 tol = pf2_fma(pf2_of(4.0f * kRel * f.a), oo + rr, pf2_of(1e-30f));
+    const pf2 dt = __builtin_elementwise_max(disc, pf2_of(0.0f)) + tol;
+    const pf2 sq = pf2{__builtin_amdgcn_sqrtf(dt.x), __builtin_amdgcn_sqrtf(dt.y)} * pf2_of(1.0f + kRel);
+    // sphere_et: kRel (2 |b| + dn r + 3 sq) ia + 1e-30
+    const pf2 e0 = pf2_fma(pf2_of(3.0f), sq, pf2_fma(pf2_of(f.dn), r, pf2_of(2.0f) * pf2_abs(b)));
+    const pf2 et = pf2_fma(e0, pf2_of(kRel * f.ia), pf2_of(1e-30f));
+    const pf2 far = pf2_fma((sq - b) * pf2_of(f.ia), pf2_of(1.0f + kRel), et);
+    const pf2 r1 = (-b - sq) * pf2_of(f.ia);
+    const pf2 lo = pf2_fma(-pf2_abs(r1), pf2_of(kRel), r1) - et;
+    m0 = !(disc.x < -tol.x) && !(far.x < kTminLo);
+    m1 = !(disc.y < -tol.y) && !(far.y < kTminLo);
+    lo0 = lo.x;
+    lo1 = lo.y;
+}
+
+template <int CODE>
+__device__ __forceinline__ void aquad_maybe_pre2(const float* v, const FRay& f, const QuadPreRay& qr, bool& m0,
+                                                 bool& m1, float& lo0, float& lo1) {
+    RT_FP32_FUSED
+    constexpr int a = (CODE - 1) % 3, vflag = (CODE - 1) / 3;
+    constexpr int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+    const pf2 xa = {v[0], v[1]}, sv = {v[2], v[3]}, su = {v[4], v[5]}, nq1 = {v[6], v[7]}, nq2 = {v[8], v[9]};
+    const pf2 nsv = {v[10], v[11]}, nsu = {v[12], v[13]};
+    const float qk = v[14];
+    const pf2 t = pf2_fma(xa, pf2_of(f.inv[a]), pf2_of(f.noi[a]));
+    const float an = ::fabsf(f.noi[a]);
+    const pf2 tn = {::fabsf(t.x) + an, ::fabsf(t.y) + an};  // source modifiers, no masks
+    const pf2 et = pf2_fma(pf2_of(kEt), tn, pf2_of(1e-30f));
+    const pf2 te = t + et;
+    const pf2 lo = t - et;
+    const pf2 alpha = pf2_fma(pf2_fma(t, pf2_of(f.d[ia]), pf2_of(f.o[ia])), sv, nq1);  // alpha - 1/2
+    const pf2 beta = pf2_fma(pf2_fma(t, pf2_of(f.d[ib]), pf2_of(f.o[ib])), su, nq2);   // beta - 1/2
+    const pf2 dp = pf2_fma(tn, pf2_of(qr.c1), pf2_of(qr.c0 + qk));
+    const pf2 wa = pf2_fma(nsv, dp, pf2_abs(alpha));
+    const pf2 wb = pf2_fma(nsu, dp, pf2_abs(beta));
+    const bool par = !(::fabsf(f.d[a]) > f.pthr);  // near-parallel: the exact test decides
+    m0 = par || (!(te.x < kTminLo) && !(wa.x > kWin) && !(wb.x > kWin));
+    m1 = par || (!(te.y < kTminLo) && !(wa.y > kWin) && !(wb.y > kWin));
+    lo0 = par ? kTminLo : lo.x;
+    lo1 = par ? kTminLo : lo.y;
+}
+
 // The brute-force pass's per-lane candidate bounds live in fp16 LDS columns (half the
 // LDS of fp32: room for more pool slots). A stored bound must stay a lower bound: clamped
 // at 0 (every hit has t > 0.001) and converted toward zero (v_cvt_pkrtz: round down for
-// non-negative values; above 65504 it saturates to 65504, still below); NaN stays NaN
-// (such a candidate is always tested).
+// non-negative values; above 65504 it saturates to 65504, still below). A NaN bound stores
+// 0, the smallest bound: such a candidate is tested before any other and never ends the
+// nearest-first loop (0 <= every best t), so it is always tested.
+__device__ __forceinline__ float lot_clamp(float lo) { return lo > 0.0f ? lo : 0.0f; }
 __device__ __forceinline__ uint16_t lot_store(float lo) {
-    const float v = lo != lo ? lo : ::fmaxf(lo, 0.0f);
-    const auto h = __builtin_amdgcn_cvt_pkrtz(v, 0.0f);
+    const auto h = __builtin_amdgcn_cvt_pkrtz(lot_clamp(lo), 0.0f);
     return __builtin_bit_cast(uint16_t, h[0]);
 }
 __device__ __forceinline__ float lot_load(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
@@ -1392,23 +1456,55 @@ struct NoHook {
 template <class Real, bool COUNT, class Hook = NoHook>
 __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_prims, const RayK<Real>& r, Real& t_hit,
                                                     uint16_t* lot, uint32_t* cnt, Hook after_prefilter = Hook()) {
+    (void)n_prims;  // the records (S.n_pre) cover the primitives; the mask holds their slots
     const FRay f = make_fray(r.o, r.d);
     const QuadPreRay qr = quad_pre_ray(f);
     uint32_t mask = 0u;
-    for (int k = 0; k < n_prims; ++k) {
+    for (int g = 0; g < S.n_pre; ++g) {
         // one scalar load (wave-uniform). (Round 4 tried issuing the next record's load an
         // iteration ahead: the two records' SGPRs pushed the pool kernel into SGPR spills,
         // Cornell path kernel 13.93 -> 14.65 ms; profiles/r04/ahead/.)
-        const RtPre q = ld_uniform(S.gpre, k);
+        const RtPre q = ld_uniform(S.gpre, g);
+        const int kind = q.head & 0xff, k0 = (q.head >> 8) & 0xff, k1 = q.head >> 16;
+        const float* v = q.f;
+        if (kind >= PRE_SPHERE2) {  // a pair
+            bool m0, m1;
+            float lo0, lo1;
+            if (kind == PRE_SPHERE2) {
+                if (COUNT) cnt[CT_SPHERE] += 2;
+                sphere_maybe2(v, f, m0, m1, lo0, lo1);
+            } else {
+                if (COUNT) cnt[CT_QUAD] += 2;
+                switch (kind - PRE_QUAD2) {
+                    case 1: aquad_maybe_pre2<1>(v, f, qr, m0, m1, lo0, lo1); break;
+                    case 2: aquad_maybe_pre2<2>(v, f, qr, m0, m1, lo0, lo1); break;
+                    case 3: aquad_maybe_pre2<3>(v, f, qr, m0, m1, lo0, lo1); break;
+                    case 4: aquad_maybe_pre2<4>(v, f, qr, m0, m1, lo0, lo1); break;
+                    case 5: aquad_maybe_pre2<5>(v, f, qr, m0, m1, lo0, lo1); break;
+                    default: aquad_maybe_pre2<6>(v, f, qr, m0, m1, lo0, lo1); break;
+                }
+            }
+            // both bounds in one conversion. (The halves are taken as integer bits: with h[1]
+            // stored directly this compiler stored the LOW half for both.)
+            const uint32_t hw = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(lot_clamp(lo0), lot_clamp(lo1)));
+            if (m0) {
+                lot[k0 * kStackStride] = (uint16_t)hw;
+                mask |= 1u << k0;
+            }
+            if (m1) {
+                lot[k1 * kStackStride] = (uint16_t)(hw >> 16);
+                mask |= 1u << k1;
+            }
+            continue;
+        }
         float lo;
         bool maybe;
-        if (q.kind == PRE_SPHERE) {
+        if (kind == PRE_SPHERE) {
             if (COUNT) cnt[CT_SPHERE]++;
-            maybe = sphere_maybe(make_float4(q.f[0], q.f[1], q.f[2], q.f[3]), f, __builtin_inff(), lo);
-        } else if (q.kind != PRE_OTHER) {
+            maybe = sphere_maybe(make_float4(v[0], v[1], v[2], v[3]), f, __builtin_inff(), lo);
+        } else if (kind != PRE_OTHER) {
             if (COUNT) cnt[CT_QUAD]++;
-            const float* v = q.f;
-            switch (q.kind) {
+            switch (kind) {
                 case 1: maybe = aquad_maybe_pre<1>(v, f, qr, lo); break;
                 case 2: maybe = aquad_maybe_pre<2>(v, f, qr, lo); break;
                 case 3: maybe = aquad_maybe_pre<3>(v, f, qr, lo); break;
@@ -1417,11 +1513,11 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
                 default: maybe = aquad_maybe_pre<6>(v, f, qr, lo); break;
             }
         } else {
-            maybe = prim_maybe<COUNT>(ld_uniform(S.gprims, k), f, lo, cnt);
+            maybe = prim_maybe<COUNT>(ld_uniform(S.gprims, k0), f, lo, cnt);
         }
         if (maybe) {
-            lot[k * kStackStride] = lot_store(lo);
-            mask |= 1u << k;
+            lot[k0 * kStackStride] = lot_store(lo);
+            mask |= 1u << k0;
         }
     }
     after_prefilter();
@@ -1434,15 +1530,13 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
         cnt[CT_CAND2] += __popc(mask) >= 2 ? 1u : 0u;
     }
     while (mask != 0u) {
-        // nearest remaining candidate. A NaN bound orders first (as if -inf): it is
-        // selected before any finite bound and `lb > thi` is false for it, so it is
-        // always tested exactly and never ends the loop early.
+        // nearest remaining candidate (stored bounds are never NaN: lot_store)
         int kb = __builtin_ctz(mask);
         float lb = lot_load(lot[kb * kStackStride]);
         for (uint32_t m = mask & (mask - 1u); m != 0u; m &= m - 1u) {
             const int k = __builtin_ctz(m);
             const float l = lot_load(lot[k * kStackStride]);
-            if ((l < lb || l != l) && lb == lb) {
+            if (l < lb) {
                 lb = l;
                 kb = k;
             }

@@ -169,7 +169,7 @@ struct DevCtx {
     int32_t lds_words2 = 0;   // the same + [mats][lights]
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
     int32_t off_tsph2 = -1;  // leaf-order sphere records with the fp64 radius (RtLeafSph), or -1
-    int32_t off_pre = 0;
+    int32_t off_pre = 0, n_pre = 0;
     int32_t n_onb = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     // HIP events of the last launch, 3 per pass: path kernel start, path kernel
@@ -272,12 +272,25 @@ struct DevCtx {
         live = false;
     }
 
-    // RtPre (scene.hpp) of every primitive, from its RtPrim fields
-    static std::vector<RtPre> prefilter_records(const std::vector<RtPrim>& prims) {
-        std::vector<RtPre> out(prims.size());
+    // The RtPre records (scene.hpp) of the brute-force pre-filter pass, from the RtPrim fields:
+    // spheres in pairs, axis-aligned quads in pairs of one axis code, the rest (an odd one out,
+    // planar quads, planes) one per record. The pass sets each primitive's candidate bit and
+    // bound by its slot, so the records' order is free; pairs come first. Sets *n_rec.
+    static std::vector<RtPre> prefilter_records(const std::vector<RtPrim>& prims, int32_t* n_rec) {
+        struct One {
+            int kind;  // PRE_SPHERE, axis code 1..6, PRE_OTHER
+            float f[6];
+        };
+        std::vector<RtPre> out;
+        *n_rec = 0;
+        if (prims.size() > (size_t)kBruteMaxPrims) {  // closest_hit_brute_nf runs up to kBruteMaxPrims
+            out.resize(1);
+            return out;
+        }
+        std::vector<One> one(prims.size());
         for (size_t k = 0; k < prims.size(); ++k) {
             const RtPrim& p = prims[k];
-            RtPre q{};
+            One q{};
             int32_t code = 0;
             std::memcpy(&code, &p.g4[3], sizeof code);
             if (p.type == PRIM_SPHERE) {
@@ -296,12 +309,52 @@ struct DevCtx {
                 q.f[4] = (float)(-(double)p.g0[ib] * asu - 0.5);
                 constexpr double kRelPre = 1e-5;  // pt_kernel.hpp kRel
                 q.f[5] = (float)(kRelPre * std::max(std::fabs((double)p.g0[ia]), std::fabs((double)p.g0[ib])) * (1.0 + 1e-6));
-                q.f[6] = 0.0f;
             } else {
                 q.kind = PRE_OTHER;
             }
-            out[k] = q;
+            one[k] = q;
         }
+        std::vector<bool> used(prims.size(), false);
+        auto head = [](int kind, size_t k0, size_t k1) { return (int32_t)(kind | (int)k0 << 8 | (int)k1 << 16); };
+        for (size_t k0 = 0; k0 < prims.size(); ++k0) {  // pairs of one kind (sphere / axis code)
+            const int kind = one[k0].kind;
+            if (used[k0] || kind == PRE_OTHER) continue;
+            size_t k1 = k0 + 1;
+            while (k1 < prims.size() && (used[k1] || one[k1].kind != kind)) ++k1;
+            if (k1 == prims.size()) continue;
+            used[k0] = used[k1] = true;
+            const One &a = one[k0], &b = one[k1];
+            RtPre r{};
+            if (kind == PRE_SPHERE) {
+                for (int i = 0; i < 4; ++i) {
+                    r.f[2 * i] = a.f[i];
+                    r.f[2 * i + 1] = b.f[i];
+                }
+                r.f[8] = a.f[3] * a.f[3];
+                r.f[9] = b.f[3] * b.f[3];
+                r.head = head(PRE_SPHERE2, k0, k1);
+            } else {
+                for (int i = 0; i < 5; ++i) {
+                    r.f[2 * i] = a.f[i];
+                    r.f[2 * i + 1] = b.f[i];
+                }
+                r.f[10] = -std::fabs(a.f[1]);
+                r.f[11] = -std::fabs(b.f[1]);
+                r.f[12] = -std::fabs(a.f[2]);
+                r.f[13] = -std::fabs(b.f[2]);
+                r.f[14] = std::max(a.f[5], b.f[5]);
+                r.head = head(PRE_QUAD2 + kind, k0, k1);
+            }
+            out.push_back(r);
+        }
+        for (size_t k = 0; k < prims.size(); ++k) {  // the rest, one per record
+            if (used[k]) continue;
+            RtPre r{};
+            for (int i = 0; i < 6; ++i) r.f[i] = one[k].f[i];
+            r.head = head(one[k].kind, k, 0);
+            out.push_back(r);
+        }
+        *n_rec = (int32_t)out.size();
         if (out.empty()) out.resize(1);  // 16-byte multiple, never empty
         return out;
     }
@@ -332,7 +385,7 @@ struct DevCtx {
         append(blob, onbs, &off_onbs);
         lds_words2 = (int32_t)(blob.size() / 16);
         append(blob, build.nodes, &off_nodes);
-        append(blob, prefilter_records(build.prims), &off_pre);
+        append(blob, prefilter_records(build.prims, &n_pre), &off_pre);
         off_tsph2 = -1;
         if (!build.tsph2.empty()) append(blob, build.tsph2, &off_tsph2);
         hip_check(hipMalloc(&d_blob, std::max<size_t>(blob.size(), 16)), "hipMalloc");
@@ -393,6 +446,7 @@ struct DevCtx {
         S.prims = reinterpret_cast<const RtPrim*>(b + off_prims);
         S.gprims = S.prims;
         S.gpre = reinterpret_cast<const RtPre*>(b + off_pre);
+        S.n_pre = n_pre;
         S.tprims = reinterpret_cast<const int32_t*>(b + off_tprims);
         S.off_tprims = off_tprims;
         S.tsph = reinterpret_cast<const float4*>(b + off_tsph);

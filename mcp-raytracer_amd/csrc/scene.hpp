@@ -102,18 +102,25 @@ struct alignas(16) RtMat {
 };
 static_assert(sizeof(RtMat) == 64, "RtMat must be 64 bytes");
 
-// Compact brute-force pre-filter record per primitive (slot order): everything the
-// fp32 pre-filter of a sphere or an axis-aligned quad reads, in one 32-byte scalar
-// load (the full RtPrim takes two dependent loads for a quad: its type, then its
-// axis code). kind: PRE_SPHERE {cx, cy, cz, r}; 1..6 = axis code {x_a of the plane (D / n[a]),
-// sv = +-w[a]*v[iv], su = +-w[a]*u[iu], -Q[ia]*sv - 1/2, -Q[ib]*su - 1/2, kRel max(|Q[ia]|, |Q[ib]|), 0}
-// (scene.cpp encode_axis_quad, rt_api.cpp prefilter_records); PRE_OTHER: read the RtPrim.
-enum : int32_t { PRE_SPHERE = 0, PRE_OTHER = 7 };
+// Compact brute-force pre-filter record: everything the fp32 pre-filter of one primitive, or of
+// a PAIR of primitives evaluated together in packed fp32 (v_pk_fma_f32: two spheres, or two
+// axis-aligned quads of one axis code, which share every ray operand), reads in one 64-byte
+// scalar load (the full RtPrim takes two dependent loads for a quad: its type, then its axis
+// code). head = kind | k0 << 8 | k1 << 16 (the primitives' slots; k1 only for pairs), last so
+// that the pairs' floats sit in aligned SGPR pairs.
+//   PRE_SPHERE {cx, cy, cz, r}; 1..6 = axis code {x_a of the plane (D / n[a]), sv = +-w[a]*v[iv],
+//   su = +-w[a]*u[iu], -Q[ia]*sv - 1/2, -Q[ib]*su - 1/2, kRel max(|Q[ia]|, |Q[ib]|)};
+//   PRE_OTHER: read the RtPrim;
+//   PRE_SPHERE2 {cx0, cx1, cy0, cy1, cz0, cz1, r0, r1, r0^2, r1^2};
+//   PRE_QUAD2 + code {x_a, sv, su, -Q[ia]*sv - 1/2, -Q[ib]*su - 1/2, -|sv|, -|su|} as element pairs,
+//   then max(kRel max(|Q[ia]|, |Q[ib]|)) of the two.
+// (scene.cpp encode_axis_quad, rt_api.cpp prefilter_records)
+enum : int32_t { PRE_SPHERE = 0, PRE_OTHER = 7, PRE_SPHERE2 = 8, PRE_QUAD2 = 8 /* + code 1..6 */ };
 struct alignas(16) RtPre {
-    int32_t kind;
-    float f[7];
+    float f[15];
+    int32_t head;
 };
-static_assert(sizeof(RtPre) == 32, "RtPre must be 32 bytes");
+static_assert(sizeof(RtPre) == 64, "RtPre must be 64 bytes");
 
 struct alignas(16) RtLight {
     int32_t prim;

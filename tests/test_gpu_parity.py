@@ -440,6 +440,70 @@ def test_axis_quad_edges_and_corners(rt, oracle, gpu):
     assert (c[:, 0] > 0).mean() > 0.5
 
 
+def _pair_scene():
+    """16 primitives for the brute-force pre-filter's records (rt_api.cpp prefilter_records):
+    axis-aligned quads of all six axis codes (u / v swapped gives the second code of an axis),
+    three of one code (a pair and a single), two of another on the same plane, five spheres (two
+    pairs and a single, one of them a light), a tilted quad and a plane (single records that
+    read the RtPrim)."""
+    m = {"type": "lambert", "color": [0.7, 0.6, 0.5]}
+    quads = [
+        ((-1.5, -1, -1), (0, 2, 0), (0, 0, 2)), ((1.5, -1, 1), (0, 2, 0), (0, 0, -2)),       # x, one code
+        ((0.2, -0.5, -0.5), (0, 0, 1), (0, 1, 0)),                                            # x, swapped
+        ((-1.5, -1, -1), (3, 0, 0), (0, 0, 2)), ((-1.5, 1.2, 1), (3, 0, 0), (0, 0, -2)),      # y
+        ((-0.3, 0.99, -0.3), (0.6, 0, 0), (0, 0, 0.6)),                                       # y, same code: 3rd
+        ((-1.5, -1, -1.2), (3, 0, 0), (0, 2.2, 0)), ((-1.5, -1, -1.2), (0, 2.2, 0), (3, 0, 0)),  # z, both codes
+        ((-1.0, -0.2, 0.4), (0.5, 0, 0), (0, 0.5, 0)),                                        # z, 2nd of a code
+    ]
+    objs = [{"type": "quad", "pos": list(q), "u": list(u), "v": list(v), "material": m} for q, u, v in quads]
+    objs[5]["light"] = True
+    objs[5]["material"] = {"type": "light", "emit": [8, 8, 8]}
+    for k, (c, r) in enumerate([((-0.6, -0.6, -0.3), 0.35), ((0.6, -0.7, 0.2), 0.3), ((0.0, 0.3, -0.6), 0.25),
+                                ((0.9, 0.5, 0.5), 0.2), ((-0.9, 0.6, 0.6), 0.15)]):
+        mat = {"type": "glass", "ior": 1.5} if k == 1 else m
+        objs.append({"type": "sphere", "pos": list(c), "r": r, "material": mat})
+    objs.append({"type": "quad", "pos": [0.3, -0.8, -0.9], "u": [0.4, 0.3, 0.1], "v": [-0.1, 0.2, 0.5],
+                 "material": m})
+    objs.append({"type": "plane", "pos": [0, -1.05, 0], "u": [1, 0, 0], "v": [0, 0, -1], "material": m})
+    return {"camera": {"vfov": 60, "from": [0, 0, 3.5], "at": [0, 0, 0], "up": [0, 1, 0],
+                       "background": {"type": "gradient", "top": [0.5, 0.7, 1.0], "bottom": [1, 1, 1]}},
+            "objects": objs}
+
+
+def test_prefilter_pair_records_match_oracle(rt, oracle, gpu):
+    """The brute-force pass evaluates spheres and same-code axis quads two at a time (packed
+    fp32). Hits from inside and outside the box, rays leaving the walls and spheres (self-hit
+    rejection), near-parallel rays and window edges, then a rendered image, against the oracle."""
+    sd = _pair_scene()
+    assert len(sd["objects"]) == 16
+    rng = np.random.default_rng(21)
+    n = 6000
+    o = rng.uniform(-1.4, 1.4, (n, 3))
+    o[: n // 4] = rng.uniform(-60, 60, (n // 4, 3))
+    d = rng.normal(size=(n, 3))
+    # rays starting on the walls x = -1.5 / y = -1 / z = -1.2 and on a sphere, leaving them
+    k = n // 8
+    o[k:2 * k, 0] = -1.5
+    d[k:2 * k, 0] = np.abs(d[k:2 * k, 0])
+    o[2 * k:3 * k, 1] = -1.0
+    o[3 * k:4 * k, 2] = -1.2
+    u = rng.normal(size=(k, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    o[4 * k:5 * k] = np.float64([-0.6, -0.6, -0.3]) + 0.35 * u
+    # near-parallel to the y planes, and aimed at quad edges
+    d[5 * k:6 * k, 1] = d[5 * k:6 * k, 1] * 1e-4
+    o = o.astype(np.float32)
+    d = d.astype(np.float32)
+    c = _hit_equal(rt, oracle, sd, o, d)
+    assert (c[:, 0] > 0).mean() > 0.5
+    ro = {"width": 48, "samples": 8, "depth": 10, **NOADAPT}
+    orc = oracle.render(sd, ro)
+    for prec_trav in ("brute", "auto"):
+        _, rgb, rad, st = _render_gpu(rt, sd, {**ro, "traversal": prec_trav})
+        assert_identical(rad, rgb, orc["radiance"], orc["rgb"], f"pair scene {prec_trav}")
+        assert_stats_identical(st, orc["stats"])
+
+
 @pytest.mark.parametrize("cfg", [{"type": "cornell"}, {"type": "spheres", "options": {"count": 500, "seed": 42}},
                                  {"type": "spheres", "options": {"count": 6000, "seed": 9}}],
                          ids=["cornell", "spheres500", "spheres6000"])
