@@ -636,6 +636,13 @@ __device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
 // on an infinite bound, which fminf / fmaxf ignore), tf = min(thi, 0) >= 0, and the test
 // accepts every box - still the reference's hit, at brute-force cost (|o| > ~1e7 only).
 __device__ __forceinline__ float slab_t(float b, const FRay& f, int a) { return __builtin_fmaf(b, f.inv[a], f.noi[a]); }
+// Two-float vectors for packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: one instruction
+// for both elements, the same IEEE operation on each); operand pairs in aligned register pairs,
+// broadcast scalars by op_sel.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pf2_of(float x) { return pf2{x, x}; }
+__device__ __forceinline__ pf2 pf2_fma(pf2 a, pf2 b, pf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ pf2 pf2_abs(pf2 a) { return __builtin_elementwise_abs(a); }
 __device__ __forceinline__ bool slab_accept(float tn, float tf, const FRay& f) {
     return tn <= __builtin_fmaf(tf, 1.000002f, f.eps);
 }
@@ -754,7 +761,8 @@ __device__ __forceinline__ int t4_step(const DevScene& S, int ref, const FRay& f
     for (int c = 0; c < 4; ++c) {
         // near / far plane t per axis: the same two values min / max would pick (fma is monotone
         // in b for a fixed inv, so the sign of inv orders the planes; a NaN plane - an infinite
-        // bound times inv = 0 - is ignored by fmaxf / fminf either way)
+        // bound times inv = 0 - is ignored by fmaxf / fminf either way). (Round 6: the 24 plane
+        // FMAs as 12 packed v_pk_fma_f32 ran 1.2-2.4 % slower on the BVH configs, profiles/r06/pairs/.)
         float tn = kTminLo, tf = thi;
         if (nf) {
             tn = ::fmaxf(::fmaxf(::fmaxf(slab_t(bn[0][c], f, 0), slab_t(bn[1][c], f, 1)), slab_t(bn[2][c], f, 2)), tn);
@@ -1376,10 +1384,6 @@ __device__ __forceinline__ bool aquad_maybe_pre(const float* v, const FRay& f, c
 // broadcast with op_sel). Branch-free: both results are computed and masked. The margins are
 // the single tests' (a filter may round differently as long as it stays conservative; the
 // pair's window margin uses the larger qk of the two).
-typedef float pf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ pf2 pf2_of(float x) { return pf2{x, x}; }
-__device__ __forceinline__ pf2 pf2_fma(pf2 a, pf2 b, pf2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ pf2 pf2_abs(pf2 a) { return __builtin_elementwise_abs(a); }
 
 __device__ __forceinline__ void sphere_maybe2(const float* v, const FRay& f, bool& m0, bool& m1, float& lo0,
                                               float& lo1) {
