@@ -42,6 +42,8 @@ struct DevScene {
     const RtPrim* __restrict__ gprims;  // always the global copy (scalar-load reads)
     const RtPre* __restrict__ gpre;     // brute-force pre-filter records (global, scalar-load reads)
     int32_t n_pre;                      // ... and their count (pairs count once)
+    const RtExact* __restrict__ xrec;   // brute-force exact-test records (LDS when resident), slot order
+    int32_t off_xrec;                   // byte offset of xrec in the blob
     const int32_t* __restrict__ tprims; // fast-traversal leaves -> primitive slots (LDS when resident)
     const float4* __restrict__ tsph;    // per tprims entry: sphere {centre, fp32 radius} or NaNs (LDS when resident)
     const RtMat* __restrict__ mats;
@@ -1324,6 +1326,76 @@ __device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Rea
     return true;
 }
 
+// prim_exact_fused from the primitive's RtExact record: the same operations on the same
+// operands (the record holds the RtPrim fields aquad_t_c / sphere_t read), loaded up front.
+// PRE_OTHER records take prim_exact on the RtPrim `p` (read only there).
+// The record's two 16-byte loads, issued together and waited for once: the empty asm takes the
+// loaded words as its operands, so the loads cannot sink to their first uses (the compiler did
+// that: kind, then s0, then the fields - dependent round trips again).
+__device__ __forceinline__ RtExact xrec_load(const RtExact* px) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4* src = reinterpret_cast<const u4*>(px);
+    u4 w0 = src[0], w1 = src[1];
+    __asm__ volatile("" : "+v"(w0), "+v"(w1));
+    struct W {
+        u4 a, b;
+    } w{w0, w1};
+    return __builtin_bit_cast(RtExact, w);
+}
+template <class Real>
+__device__ __forceinline__ bool prim_exact_rec(const RtExact& x, const RtPrim& p, const RayK<Real>& r, Real& t) {
+    const Real inf = (Real)__builtin_inf();
+    const int code = x.kind & 7;
+    const bool sph = code == PRE_SPHERE;
+    if (code == PRE_OTHER) return prim_exact<Real>(p, r, t);
+    const Real s0 = (Real)x.s0;  // the JS double, or the fp32 mode's (float) s0 = RtPrim g0[3]
+    Real num, den, halfB = (Real)0, sq = (Real)0;
+    float o1 = 0.f, d1 = 0.f, o2 = 0.f, d2 = 0.f;
+    if (sph) {
+        const V3 c = V3{x.f[0], x.f[1], x.f[2]};
+        const V3 oc = sub(r.o, c);
+        halfB = dot<Real>(oc, r.d);
+        const Real cc = len2<Real>(oc) - s0 * s0;
+        const Real disc = halfB * halfB - r.a * cc;
+        if (disc < (Real)0) return false;
+        sq = m_sqrt(disc);
+        num = -halfB - sq;
+        den = r.a;
+    } else {
+        const int a = (int)((aquad_axes(0) >> (2 * code)) & 3u);
+        const int ia = (int)((aquad_axes(1) >> (2 * code)) & 3u);
+        const int ib = (int)((aquad_axes(2) >> (2 * code)) & 3u);
+        const V3 o3 = r.o, d3 = r.d;
+        const float oa = sel3(o3.x, o3.y, o3.z, a), da = sel3(d3.x, d3.y, d3.z, a);
+        o1 = sel3(o3.x, o3.y, o3.z, ia);
+        d1 = sel3(d3.x, d3.y, d3.z, ia);
+        o2 = sel3(o3.x, o3.y, o3.z, ib);
+        d2 = sel3(d3.x, d3.y, d3.z, ib);
+        if (!(::isfinite(o1) && ::isfinite(d1) && ::isfinite(o2) && ::isfinite(d2))) return false;
+        const Real na = (x.kind & kExactNegNa) ? (Real)-1 : (Real)1;  // n[a], exactly +-1
+        den = na * (Real)da;
+        if (m_abs(den) < (Real)1e-8) return false;
+        num = s0 - na * (Real)oa;
+    }
+    Real q = num / den;
+    if (sph) {
+        if (!(K<Real>::TMIN < q && q < inf)) {
+            q = (-halfB + sq) / r.a;
+            if (!(K<Real>::TMIN < q && q < inf)) return false;
+        }
+    } else {
+        if (!(K<Real>::TMIN < q && q < inf)) return false;
+        const float ph1 = (o1 + (float)((Real)d1 * q)) - x.f[0];
+        const float ph2 = (o2 + (float)((Real)d2 * q)) - x.f[1];
+        const Real sw = (Real)x.f[2];
+        const Real alpha = sw * (Real)(ph1 * x.f[3]);
+        const Real beta = sw * (Real)(ph2 * x.f[4]);
+        if (alpha < (Real)0 || alpha > (Real)1 || beta < (Real)0 || beta > (Real)1) return false;
+    }
+    t = q;
+    return true;
+}
+
 // The brute-force pass's axis-quad pre-filter over an RtPre record {x_a, sv, su, -Q[ia] sv - 1/2,
 // -Q[ib] su - 1/2, kRel qm} (qm = max(|Q[ia]|, |Q[ib]|)). The plane's t comes from the ray's slab
 // constants, t = fma(x_a, inv[a], noi[a]), instead of a reciprocal of n.d per quad, and alpha - 1/2,
@@ -1552,7 +1624,7 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
             if (++n_exact == 2) cnt[CT_EXACT2]++;
         }
         Real t;
-        const bool hit = prim_exact_fused<Real>(S.prims[kb], ray_at_use<Real>(r), t);
+        const bool hit = prim_exact_rec<Real>(xrec_load(S.xrec + kb), S.prims[kb], ray_at_use<Real>(r), t);
         if (hit && (t < best_t || (t == best_t && kb < best))) {
             best_t = t;
             best = kb;
@@ -2235,6 +2307,7 @@ __device__ __forceinline__ DevScene scene_view(const DevScene& S0, int* lds_stac
         S.tprims = reinterpret_cast<const int32_t*>(b + S0.off_tprims);
         S.tsph = reinterpret_cast<const float4*>(b + S0.off_tsph);
         S.prims = reinterpret_cast<const RtPrim*>(b + S0.off_prims);
+        S.xrec = reinterpret_cast<const RtExact*>(b + S0.off_xrec);
         if (LDSS == 2) {
             S.mats = reinterpret_cast<const RtMat*>(b + S0.off_mats);
             S.lights = reinterpret_cast<const RtLight*>(b + S0.off_lights);

@@ -169,7 +169,7 @@ struct DevCtx {
     int32_t lds_words2 = 0;   // the same + [mats][lights]
     int32_t off_prims = 0, off_mats = 0, off_lights = 0, off_nodes = 0, off_tprims = 0, off_tsph = 0, off_onbs = 0;
     int32_t off_tsph2 = -1;  // leaf-order sphere records with the fp64 radius (RtLeafSph), or -1
-    int32_t off_pre = 0, n_pre = 0;
+    int32_t off_pre = 0, n_pre = 0, off_xrec = 0;
     int32_t n_onb = 0;
     int lds_max = 64 * 1024;  // dynamic LDS bytes a workgroup may use on this device
     // HIP events of the last launch, 3 per pass: path kernel start, path kernel
@@ -270,6 +270,40 @@ struct DevCtx {
         n_passes = 0;
         (void)hipSetDevice(prev);
         live = false;
+    }
+
+    // The RtExact records (scene.hpp) of a brute-force scene's primitives (empty above
+    // kBruteMaxPrims: only closest_hit_brute_nf reads them)
+    static std::vector<RtExact> exact_records(const std::vector<RtPrim>& prims) {
+        std::vector<RtExact> out;
+        if (prims.size() > (size_t)kBruteMaxPrims) return out;
+        for (const RtPrim& p : prims) {
+            RtExact x{};
+            int32_t code = 0;
+            std::memcpy(&code, &p.g4[3], sizeof code);
+            x.s0 = p.s0;
+            x.kind = PRE_OTHER;
+            // the fp32 mode's radius / D is (float)s0; a primitive whose g0[3] is not (NaN
+            // fields, say) keeps the RtPrim path
+            const bool s0f_ok = (float)p.s0 == p.g0[3];
+            if (p.type == PRIM_SPHERE && s0f_ok) {
+                x.kind = PRE_SPHERE;
+                for (int i = 0; i < 3; ++i) x.f[i] = p.g0[i];
+            } else if (p.type == PRIM_QUAD && code >= 1 && code <= 6 && s0f_ok) {
+                const int a = (code - 1) % 3, vflag = (code - 1) / 3;
+                const int ia = vflag ? (a + 1) % 3 : (a + 2) % 3, ib = vflag ? (a + 2) % 3 : (a + 1) % 3;
+                if (p.g3[a] == 1.0f || p.g3[a] == -1.0f) {  // always so (a one-component unit normal)
+                    x.kind = code | (p.g3[a] < 0.0f ? kExactNegNa : 0);
+                    x.f[0] = p.g0[ia];
+                    x.f[1] = p.g0[ib];
+                    x.f[2] = p.g3[3];
+                    x.f[3] = p.g2[3];
+                    x.f[4] = p.g1[3];
+                }
+            }
+            out.push_back(x);
+        }
+        return out;
     }
 
     // The RtPre records (scene.hpp) of the brute-force pre-filter pass, from the RtPrim fields:
@@ -378,6 +412,7 @@ struct DevCtx {
         append(blob, build.tprims, &off_tprims);
         append(blob, build.tsph, &off_tsph);
         append(blob, build.prims, &off_prims);
+        append(blob, exact_records(build.prims), &off_xrec);
         lds_words = (int32_t)(blob.size() / 16);
         append(blob, build.mats, &off_mats);
         append(blob, build.lights, &off_lights);
@@ -447,6 +482,8 @@ struct DevCtx {
         S.gprims = S.prims;
         S.gpre = reinterpret_cast<const RtPre*>(b + off_pre);
         S.n_pre = n_pre;
+        S.xrec = reinterpret_cast<const RtExact*>(b + off_xrec);
+        S.off_xrec = off_xrec;
         S.tprims = reinterpret_cast<const int32_t*>(b + off_tprims);
         S.off_tprims = off_tprims;
         S.tsph = reinterpret_cast<const float4*>(b + off_tsph);

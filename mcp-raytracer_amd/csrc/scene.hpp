@@ -122,6 +122,21 @@ struct alignas(16) RtPre {
 };
 static_assert(sizeof(RtPre) == 64, "RtPre must be 64 bytes");
 
+// Exact-test record of a brute-force primitive (slot order; in the LDS copy beside the RtPrims):
+// every field the nearest-first pass's exact test reads, in two 16-byte loads issued together
+// (through the RtPrim they were five dependent LDS round trips: type, axis code, then the
+// type's fields). s0: the radius / D (the JS double; the fp32 mode's value is (float)s0 =
+// RtPrim g0[3]). kind as RtPre: PRE_SPHERE {centre xyz}, axis code 1..6 {Q[ia], Q[ib], +-w[a],
+// v[iv], u[iu]} (the RtPrim fields aquad_t_c reads; its n[a] is +-1 exactly, the sign in bit 3
+// of kind), PRE_OTHER (read the RtPrim).
+struct alignas(16) RtExact {
+    double s0;
+    float f[5];
+    int32_t kind;
+};
+static_assert(sizeof(RtExact) == 32, "RtExact must be 32 bytes");
+constexpr int32_t kExactNegNa = 8;  // RtExact::kind flag: n[a] = -1
+
 struct alignas(16) RtLight {
     int32_t prim;
     int32_t type;
