@@ -4,6 +4,7 @@
 Runs the section-timing build (INSTR == 2) once per configuration and prints each
 section's share of the summed wave-cycles, plus wall time of the product build.
 """
+import os
 import json
 import sys
 import time
@@ -26,6 +27,9 @@ def main():
             ("rain", 1920, 64, 16, "ref", "auto"), ("spheres100k", 1024, 4, 100, "ref", "auto")]
     if len(sys.argv) > 1:
         cfgs = [c for c in cfgs if c[0] in sys.argv[1:]]
+    if os.environ.get("RT_SECTIONS_ONLY"):  # e.g. "ref auto": only the configs of that precision / traversal
+        prec, trav = os.environ["RT_SECTIONS_ONLY"].split()
+        cfgs = [c for c in cfgs if c[4] == prec and c[5] == trav]
     for scene, width, spp, depth, prec, trav in cfgs:
         cfg, extra, _ = SCENES[scene]
         sd = rt.generate_scene_data(cfg)
