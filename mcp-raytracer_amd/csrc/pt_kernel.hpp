@@ -2593,6 +2593,11 @@ __device__ __forceinline__ bool slot_pixel(const SB& sb, const RtRegion& reg, in
     if (sb.act) {
         if (a >= sb.slots) return false;
         ls = sb.act[a];
+        // Wait for this load here, on every path. Otherwise (fixed-spp launches never take this
+        // branch) the wait-count pass kept its destination register pending on the paths around
+        // the branch, and every later write of that register - a common temporary - waited with
+        // vmcnt(0): for the sample records just stored, too.
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unchanged (gfx9 encoding)
     }
     item_pixel(reg, tiles_x, rtx, sb.tile0 + (ls >> 6), ls & 63, i, j);
     return i < endX && j < endY;
