@@ -1265,70 +1265,6 @@ __device__ __forceinline__ bool prim_exact(const RtPrim& p, const RayK<Real>& r,
     return planar_t<Real, false>(p, r, K<Real>::TMIN, inf, t);
 }
 
-// prim_exact with the sphere's root and the axis-aligned quad's plane t through ONE
-// division: lanes of a wave test different primitive types, and each type's block
-// costs the whole wave; the prologues stay per type, the division (the longest
-// piece of either) is shared. Same operations on the same operands: sphere_t's
-// (-h - sqrt(disc)) / a and aquad_t_rt's (D - n.o) / (n.d).
-template <class Real>
-__device__ __forceinline__ bool prim_exact_fused(const RtPrim& p, const RayK<Real>& r, Real& t) {
-    const Real inf = (Real)__builtin_inf();
-    const int code = aquad_code(p);
-    const bool sph = p.type == PRIM_SPHERE;
-    if (!sph && !(p.type == PRIM_QUAD && code != 0)) return prim_exact<Real>(p, r, t);
-    Real num, den, halfB = (Real)0, sq = (Real)0;
-    float o1 = 0.f, d1 = 0.f, o2 = 0.f, d2 = 0.f, q1 = 0.f, q2 = 0.f;
-    if (sph) {
-        const V3 c = ld3(p.g0);
-        const Real rad = sphere_radius<Real>(p);
-        const V3 oc = sub(r.o, c);
-        halfB = dot<Real>(oc, r.d);
-        const Real cc = len2<Real>(oc) - rad * rad;
-        const Real disc = halfB * halfB - r.a * cc;
-        if (disc < (Real)0) return false;
-        sq = m_sqrt(disc);
-        num = -halfB - sq;
-        den = r.a;
-    } else {
-        const int a = (int)((aquad_axes(0) >> (2 * code)) & 3u);
-        const int ia = (int)((aquad_axes(1) >> (2 * code)) & 3u);
-        const int ib = (int)((aquad_axes(2) >> (2 * code)) & 3u);
-        const V3 o3 = r.o, d3 = r.d;
-        const float oa = sel3(o3.x, o3.y, o3.z, a), da = sel3(d3.x, d3.y, d3.z, a);
-        o1 = sel3(o3.x, o3.y, o3.z, ia);
-        d1 = sel3(d3.x, d3.y, d3.z, ia);
-        o2 = sel3(o3.x, o3.y, o3.z, ib);
-        d2 = sel3(d3.x, d3.y, d3.z, ib);
-        q1 = sel3(p.g0[0], p.g0[1], p.g0[2], ia);
-        q2 = sel3(p.g0[0], p.g0[1], p.g0[2], ib);
-        if (!(::isfinite(o1) && ::isfinite(d1) && ::isfinite(o2) && ::isfinite(d2))) return false;
-        const Real na = (Real)sel3(p.g3[0], p.g3[1], p.g3[2], a);
-        den = na * (Real)da;
-        if (m_abs(den) < (Real)1e-8) return false;
-        num = plane_d<Real>(p) - na * (Real)oa;
-    }
-    Real q = num / den;
-    if (sph) {
-        if (!(K<Real>::TMIN < q && q < inf)) {
-            q = (-halfB + sq) / r.a;
-            if (!(K<Real>::TMIN < q && q < inf)) return false;
-        }
-    } else {
-        if (!(K<Real>::TMIN < q && q < inf)) return false;
-        const float ph1 = (o1 + (float)((Real)d1 * q)) - q1;
-        const float ph2 = (o2 + (float)((Real)d2 * q)) - q2;
-        const Real sw = (Real)p.g3[3];
-        const Real alpha = sw * (Real)(ph1 * p.g2[3]);
-        const Real beta = sw * (Real)(ph2 * p.g1[3]);
-        if (alpha < (Real)0 || alpha > (Real)1 || beta < (Real)0 || beta > (Real)1) return false;
-    }
-    t = q;
-    return true;
-}
-
-// prim_exact_fused from the primitive's RtExact record: the same operations on the same
-// operands (the record holds the RtPrim fields aquad_t_c / sphere_t read), loaded up front.
-// PRE_OTHER records take prim_exact on the RtPrim `p` (read only there).
 // The record's two 16-byte loads, issued together and waited for once: the empty asm takes the
 // loaded words as its operands, so the loads cannot sink to their first uses (the compiler did
 // that: kind, then s0, then the fields - dependent round trips again).
@@ -1342,6 +1278,13 @@ __device__ __forceinline__ RtExact xrec_load(const RtExact* px) {
     } w{w0, w1};
     return __builtin_bit_cast(RtExact, w);
 }
+// The nearest-first pass's exact test, from the primitive's RtExact record: prim_exact's
+// operations on the same operands (the record holds the RtPrim fields aquad_t_c / sphere_t
+// read), with the sphere's root and the axis-aligned quad's plane t through ONE division -
+// lanes of a wave test different primitive types, and each type's block costs the whole wave;
+// the prologues stay per type, the division (the longest piece of either) is shared: sphere_t's
+// (-h - sqrt(disc)) / a and aquad_t_rt's (D - n.o) / (n.d). PRE_OTHER records take prim_exact
+// on the RtPrim `p` (read only there).
 template <class Real>
 __device__ __forceinline__ bool prim_exact_rec(const RtExact& x, const RtPrim& p, const RayK<Real>& r, Real& t) {
     const Real inf = (Real)__builtin_inf();
