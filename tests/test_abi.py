@@ -55,6 +55,46 @@ def test_product_kernels_do_not_spill_to_scratch(rt):
     assert max(k["vgpr"] for k in checked if re.search(r"pt_(pool|chunk)_kernel", k["name"])) <= 128
 
 
+def test_pool_kernel_trip_loop_waits_on_no_stores(rt, tmp_path):
+    """The LDS-resident pool kernels (the headline's) keep their `s_waitcnt vmcnt(0)` count at the
+    prologue's and the work hand-out's few: a vmcnt(0) in the trip loop also waits for the sample
+    records stored just before it. Round 6 found 17 such waits, inserted before writes of a register
+    the wait-count pass kept pending from the adaptive active-list load on the paths around its
+    branch (pt_kernel.hpp slot_pixel; Cornell +0.4 %, fp32 +1.3 %, adaptive +4 %)."""
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+    from raytracer_amd import _lib
+    objdump = Path("/opt/rocm/lib/llvm/bin/llvm-objdump")
+    if not objdump.exists():
+        objdump = Path(shutil.which("llvm-objdump") or "/nonexistent")
+    if not objdump.exists():
+        pytest.skip("llvm-objdump not found")
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import kernel_resources
+    counts = {}
+    for i, code in enumerate(kernel_resources.code_objects(_lib.LIB_PATH)):
+        f = tmp_path / f"co{i}.o"
+        f.write_bytes(code)
+        text = subprocess.run([str(objdump), "-d", "--no-show-raw-insn", str(f)], check=True,
+                              capture_output=True, text=True).stdout
+        name = None
+        for line in text.splitlines():
+            # pt_pool_kernel<Real, TRAV_BRUTE, LDSS 2> (the LDSS-0 instances read the scene from
+            # global memory: their vmcnt waits are the scene loads)
+            m = re.match(r"^[0-9a-f]+ <(_ZN2rt14pt_pool_kernelI[df]Li2ELi2E[^>]*)>:", line)
+            if m:
+                name = m.group(1)
+                counts[name] = 0
+            elif re.match(r"^[0-9a-f]+ <", line):
+                name = None
+            elif name and "s_waitcnt vmcnt(0)" in line:
+                counts[name] += 1
+    assert len(counts) == 2, counts  # ref and fp32
+    assert max(counts.values()) <= 8, counts
+
+
 def test_camera_info_defaults_and_merge_order(rt):
     sd = rt.generate_scene_data({"type": "cornell"})
     cam = rt.create_camera_from_scene_data(sd)  # render defaults + scene render {aspect 1, rouletteDepth 5}
