@@ -1567,9 +1567,14 @@ __device__ __forceinline__ int closest_hit_brute_nf(const DevScene& S, int n_pri
             if (++n_exact == 2) cnt[CT_EXACT2]++;
         }
         Real t;
-        // (the ray as is, not ray_at_use: its fp64 conversions may then be scheduled while the
-        // record loads are in flight - 13.14 -> 13.11 ms, profiles/r06/pairs/r06_rayhoist/)
-        const bool hit = prim_exact_rec<Real>(xrec_load(S.xrec + kb), S.prims[kb], r, t);
+        // ref precision: the ray as is, not ray_at_use - its fp64 conversions may then be
+        // scheduled while the record loads are in flight (13.14 -> 13.11 ms,
+        // profiles/r06/pairs/r06_rayhoist/). The fp32 build keeps ray_at_use: there |d|^2 may be
+        // contracted (fma) differently where make_ray is inlined, and the pool and chunked kernels
+        // must return the same hits (test_pool_kernel_equals_chunked_kernel caught 613 pixels).
+        const bool hit = sizeof(Real) == 8
+                             ? prim_exact_rec<Real>(xrec_load(S.xrec + kb), S.prims[kb], r, t)
+                             : prim_exact_rec<Real>(xrec_load(S.xrec + kb), S.prims[kb], ray_at_use<Real>(r), t);
         if (hit && (t < best_t || (t == best_t && kb < best))) {
             best_t = t;
             best = kb;
